@@ -1,0 +1,266 @@
+"""ah_rag.embeddings — text encoders and the HBM-resident dense index.
+
+Reference seams this module replaces (Yaron9/AH-RAG):
+  * the SentenceTransformer encode calls, src/ah_rag/graph/hierarchical_graph.py:655-656 (corpus,
+    normalize_embeddings=True) and :709-712 (query, cached per graph), and
+    src/ah_rag/aggregate/semantic_aggregator.py:47,71-74;
+  * the Chroma collection that stores the embeddings, hierarchical_graph.py:605-611 / :660 / :714.
+
+The encoder stays a thin PyTorch call (north star: "not re-implemented"). When
+sentence-transformers or its weights are unavailable (this image has neither), HashEncoder
+gives deterministic, L2-normalised stand-in vectors so the pipeline still runs end to end; it is
+labelled as such wherever it is used.
+
+DenseIndex is the device half: fp32 vectors go in, the index keeps them row-major in HBM as
+bf16 / f16 / f32 and answers batched top-k queries through libahr_hip.so. Nothing here falls
+back to the CPU.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+ArrayLike = Union[np.ndarray, torch.Tensor, Sequence[Sequence[float]]]
+
+DEFAULT_MODEL = "all-MiniLM-L6-v2"  # hierarchical_graph.py:50,603,705
+MODEL_DIMS = {"all-MiniLM-L6-v2": 384, "sentence-transformers/all-MiniLM-L6-v2": 384,
+              "all-mpnet-base-v2": 768, "sentence-transformers/all-mpnet-base-v2": 768}
+
+
+# ----------------------------------------------------------------------------------------------
+# Encoders
+# ----------------------------------------------------------------------------------------------
+class HashEncoder:
+    """Deterministic stand-in encoder: sha1(text) seeds a Gaussian vector, L2-normalised.
+
+    Same call shape as SentenceTransformer.encode. Identical texts give identical vectors, so
+    self-similarity is exactly 1 (the property test/test_embeddings.py:10-17 checks).
+    """
+
+    def __init__(self, model_name: str = DEFAULT_MODEL, dim: Optional[int] = None) -> None:
+        self.model_name = model_name
+        self.dim = int(dim or MODEL_DIMS.get(model_name, 384))
+
+    def get_sentence_embedding_dimension(self) -> int:
+        return self.dim
+
+    def _one(self, text: str) -> np.ndarray:
+        seed = int.from_bytes(hashlib.sha1(text.encode("utf-8")).digest()[:8], "little")
+        return np.random.default_rng(seed).standard_normal(self.dim).astype(np.float32)
+
+    def encode(self, texts: Union[str, Sequence[str]], normalize_embeddings: bool = False,
+               show_progress_bar: bool = False, batch_size: int = 32, **_: object) -> np.ndarray:
+        single = isinstance(texts, str)
+        items = [texts] if single else list(texts)
+        out = np.stack([self._one(t) for t in items]) if items else np.zeros((0, self.dim), np.float32)
+        if normalize_embeddings and len(items):
+            out = out / np.maximum(np.linalg.norm(out, axis=1, keepdims=True), 1e-12)
+        out = out.astype(np.float32)
+        return out[0] if single else out
+
+
+def load_encoder(model_name: str = DEFAULT_MODEL, dim: Optional[int] = None):
+    """SentenceTransformer(model_name) when importable and cached, else HashEncoder.
+
+    Set AHR_ENCODER=hash to force the stand-in (benchmarks use synthetic vectors anyway).
+    """
+    if os.environ.get("AHR_ENCODER", "").lower() != "hash":
+        try:
+            from sentence_transformers import SentenceTransformer  # type: ignore
+
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+            return SentenceTransformer(model_name, device=device)
+        except Exception:
+            pass
+    return HashEncoder(model_name, dim)
+
+
+# ----------------------------------------------------------------------------------------------
+# Dense index (device)
+# ----------------------------------------------------------------------------------------------
+def _as_f32_device(x: ArrayLike, device: torch.device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x.detach()
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.float32)))
+    if t.dim() == 1:
+        t = t.unsqueeze(0)
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+class DenseIndex:
+    """Row-major [capacity, dim] embedding matrix in HBM + exact batched top-k.
+
+    Rows are identified by slot numbers 0..count-1 (the caller keeps the id table).
+    dtype: "bf16" (default, north-star config), "f16", or "f32" (exact mode: every score is a
+    k-ordered fp32 fma chain, bit-exact against oracle/ahr_oracle.c).
+    """
+
+    def __init__(self, dim: int, capacity: int, dtype: str = "bf16",
+                 device: Optional[Union[int, str, torch.device]] = None) -> None:
+        if not torch.cuda.is_available():
+            raise nat.NativeLibraryError("DenseIndex needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.dim = int(dim)
+        self.capacity = int(capacity)
+        self.dtype = dtype
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        code = nat.DTYPE_CODES[dtype]
+        h = nat.ctypes.c_void_p()
+        nat.check(nat.lib().ahr_index_create(self.dim, code, self.capacity, self.device.index,
+                                             nat.ctypes.byref(h)), "ahr_index_create")
+        self._h = h
+
+    # -- lifecycle ---------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            nat.lib().ahr_index_destroy(self._h)
+            self._h = nat.ctypes.c_void_p()
+
+    def __del__(self) -> None:
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> nat.ctypes.c_void_p:
+        return self._h
+
+    def __len__(self) -> int:
+        n = nat.ctypes.c_int64()
+        nat.check(nat.lib().ahr_index_count(self._h, nat.ctypes.byref(n)), "ahr_index_count")
+        return int(n.value)
+
+    def info(self) -> dict:
+        d, dt, pd = nat.ctypes.c_int(), nat.ctypes.c_int(), nat.ctypes.c_int()
+        cap, rb = nat.ctypes.c_int64(), nat.ctypes.c_int64()
+        nat.check(nat.lib().ahr_index_info(self._h, nat.ctypes.byref(d), nat.ctypes.byref(dt),
+                                           nat.ctypes.byref(cap), nat.ctypes.byref(pd),
+                                           nat.ctypes.byref(rb)), "ahr_index_info")
+        return {"dim": d.value, "dtype": dt.value, "capacity": cap.value, "padded_dim": pd.value,
+                "row_bytes": rb.value, "count": len(self)}
+
+    # -- writes (hierarchical_graph.py:660) ----------------------------------------------------
+    def upsert(self, vectors: ArrayLike, slots: Optional[ArrayLike] = None, start: int = 0,
+               normalize: bool = False, stream: Optional[torch.cuda.Stream] = None) -> None:
+        v = _as_f32_device(vectors, self.device)
+        if v.shape[1] != self.dim:
+            raise ValueError(f"vectors have dim {v.shape[1]}, index dim is {self.dim}")
+        sl = None
+        if slots is not None:
+            sl = torch.as_tensor(np.asarray(slots, dtype=np.int64) if not isinstance(slots, torch.Tensor)
+                                 else slots, dtype=torch.int64).to(self.device).contiguous()
+            if sl.numel() != v.shape[0]:
+                raise ValueError("one slot per vector")
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_upsert(self._h, nat.ptr(v), v.shape[0], nat.ptr(sl), int(start),
+                                                 int(bool(normalize)), nat.stream_ptr(stream)),
+                      "ahr_index_upsert")
+            # keep the sources alive until the conversion kernel has consumed them
+            (stream or torch.cuda.current_stream()).synchronize()
+
+    def append(self, vectors: ArrayLike, normalize: bool = False) -> Tuple[int, int]:
+        n0 = len(self)
+        v = _as_f32_device(vectors, self.device)
+        self.upsert(v, start=n0, normalize=normalize)
+        return n0, n0 + v.shape[0]
+
+    def truncate(self, count: int = 0) -> None:
+        nat.check(nat.lib().ahr_index_truncate(self._h, int(count)), "ahr_index_truncate")
+
+    def reserve(self, max_batch: int, max_k: int = nat.AHR_MAX_K) -> None:
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_reserve(self._h, int(max_batch), int(max_k)), "ahr_index_reserve")
+
+    def read(self, start: int = 0, n: Optional[int] = None) -> torch.Tensor:
+        """Stored rows decoded to fp32 [n, dim] on the device (after dtype rounding)."""
+        total = len(self)
+        n = total - start if n is None else n
+        out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_read(self._h, int(start), int(n), nat.ptr(out), nat.stream_ptr()),
+                      "ahr_index_read")
+        return out
+
+    # -- reads (hierarchical_graph.py:714) -----------------------------------------------------
+    def query(self, queries: ArrayLike, k: int, normalize: bool = False,
+              stream: Optional[torch.cuda.Stream] = None,
+              out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Exact top-k: (scores f32 [B,k] descending, rows int32 [B,k]) on the device.
+
+        Ties order by row ascending; missing hits are (-inf, -1).
+        """
+        q = _as_f32_device(queries, self.device)
+        if q.shape[1] != self.dim:
+            raise ValueError(f"queries have dim {q.shape[1]}, index dim is {self.dim}")
+        B = q.shape[0]
+        if out is None:
+            scores = torch.empty((B, k), dtype=torch.float32, device=self.device)
+            rows = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        else:
+            scores, rows = out
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_query(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
+                                                nat.ptr(scores), nat.ptr(rows), nat.stream_ptr(stream)),
+                      "ahr_index_query")
+        return scores, rows
+
+    def query_keys(self, queries: ArrayLike, k: int, row_base: int = 0, normalize: bool = False,
+                   stream: Optional[torch.cuda.Stream] = None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Packed uint64 keys [B,k] (as int64 tensor) for cross-shard merging."""
+        q = _as_f32_device(queries, self.device)
+        B = q.shape[0]
+        keys = out if out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_query_keys(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
+                                                     int(row_base), nat.ptr(keys), nat.stream_ptr(stream)),
+                      "ahr_index_query_keys")
+        return keys
+
+
+def merge_topk_keys(keys: torch.Tensor, k: int, stream: Optional[torch.cuda.Stream] = None
+                    ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Merge per-shard key lists [n_lists, B, k_in] (or [B, n_lists, k_in]) into the top k.
+
+    Returns (scores f32 [B,k], rows int32 [B,k], keys int64 [B,k]) — the on-device merge that
+    follows the RCCL all-gather of shard results.
+    """
+    if keys.dim() != 3:
+        raise ValueError("keys must be [B, n_lists, k_in]")
+    keys = keys.contiguous()
+    B, n_lists, k_in = keys.shape
+    dev = keys.device
+    scores = torch.empty((B, k), dtype=torch.float32, device=dev)
+    rows = torch.empty((B, k), dtype=torch.int32, device=dev)
+    kout = torch.empty((B, k), dtype=torch.int64, device=dev)
+    with torch.cuda.device(dev):
+        nat.check(nat.lib().ahr_topk_merge(nat.ptr(keys), B, n_lists, k_in, int(k), nat.ptr(scores),
+                                           nat.ptr(rows), nat.ptr(kout), nat.stream_ptr(stream)),
+                  "ahr_topk_merge")
+    return scores, rows, kout
+
+
+def decode_keys(keys: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Host decode of packed keys (mirrors ahr_common.h)."""
+    k = np.asarray(keys).astype(np.uint64)
+    hi = (k >> np.uint64(32)).astype(np.uint32)
+    lo = (k & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    u = np.where(hi & np.uint32(0x80000000), hi & np.uint32(0x7FFFFFFF), ~hi).astype(np.uint32)
+    scores = u.view(np.float32).copy()
+    rows = (np.uint32(0xFFFFFFFF) - lo).astype(np.int64)
+    empty = k == 0
+    scores[empty] = -np.inf
+    rows[empty] = -1
+    return scores, rows

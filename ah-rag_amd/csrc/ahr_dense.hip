@@ -1,0 +1,813 @@
+// ahr_dense.hip — fused query x corpus inner product + exact top-k for gfx950 (MI355X).
+//
+// Replaces the ChromaDB collection behind HierarchicalGraph.search / build_vector_index
+// (reference src/ah_rag/graph/hierarchical_graph.py:605-611 create, :660 upsert, :714 query).
+// Chroma answers with an approximate HNSW walk; this kernel answers the exact question
+// (what Chroma returns when its HNSW is exhaustive), batched over B queries.
+//
+// Data layout in HBM (owned by ahr_index):
+//   corpus  [cap_pad][d_pad] row-major, dtype bf16 | f16 | f32, cap_pad % 128 == 0,
+//           rows 16-B aligned, zero padding dim..d_pad. fp32 rows are stored with each group
+//           of 8 lanes permuted to (evens | odds) so one 16-B LDS read feeds four consecutive
+//           v_mfma_f32_32x32x2_f32 k-steps (see frag_f32 below).
+//   queries [q_cap][d_pad] same format, converted from fp32 on every call.
+//   partial keys [B][n_splits][k] uint64 (ahr_common.h key format), merged by merge_kernel.
+//
+// Kernel (topk_tile_kernel): one workgroup = 4 waves (2 along rows x 2 along queries) owns a
+// 128-query block and a contiguous range of 128-row corpus tiles. Per tile it runs a K-loop of
+// 32x32 MFMAs with the corpus tile as the A operand and the query tile as B, so every lane's
+// accumulator column is ONE query and its 16 registers are 16 corpus rows of it. The score
+// tile is never stored: the epilogue compares it with the per-query k-th best key held in
+// LDS, appends the survivors to per-query LDS candidate lists, and one owner thread per query
+// folds them into a register top-k list (sorted, capacity KCAP). Survivors become rare after
+// the first tile, so the epilogue costs a compare per score.
+#include "ahr_common.h"
+#include "ahr.h"
+
+#include <algorithm>
+#include <math.h>
+
+namespace ahr {
+namespace dense {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum { DT_F32 = AHR_F32, DT_F16 = AHR_F16, DT_BF16 = AHR_BF16 };
+
+constexpr int kThreads = 256;
+constexpr int kTileRows = 128;
+constexpr int kTileQ = 128;
+constexpr int kRowBytes = 128;  // one k-tile of one row: 8 chunks of 16 B
+constexpr int kBufBytes = (kTileRows + kTileQ) * kRowBytes;  // 32 KiB: A tile, then B tile
+constexpr int kCandCap = 32;
+constexpr int kCandStride = kCandCap + 1;  // odd u64 stride: owners hit distinct banks
+
+// LDS map (bytes). The candidate lists overlay the two staging buffers: they are only live
+// between the last k-tile of a corpus tile and the first k-tile of the next one.
+constexpr int kOffBuf0 = 0;
+constexpr int kOffBuf1 = kBufBytes;
+constexpr int kOffCand = 0;
+constexpr int kCandBytes = kTileQ * kCandStride * 8;
+constexpr int kOffThrKey = 2 * kBufBytes;
+constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
+constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
+constexpr int kOffFlag = kOffCnt + kTileQ * 4;
+constexpr int kLdsBytes = kOffFlag + 16;
+static_assert(kCandBytes <= 2 * kBufBytes, "candidate overlay must fit the staging buffers");
+static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
+
+// XOR swizzle of 16-B chunks inside a 128-B row: a ds_read_b128 lane group (rows
+// {0-3,12-15,20-27} or {4-11,16-19,28-31} of a 32-row fragment, same chunk) then covers all
+// 16 slots of a 256-B bank row (conflict-free).
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+// Sorted (descending) register list of packed keys; drops the smallest on insert.
+template <int KCAP>
+__device__ __forceinline__ void list_insert(uint64_t (&L)[KCAP], uint64_t key) {
+  if (key <= L[KCAP - 1]) return;
+#pragma unroll
+  for (int j = KCAP - 1; j > 0; --j) {
+    const uint64_t prev = L[j - 1];
+    L[j] = (prev < key) ? prev : ((L[j] < key) ? key : L[j]);
+  }
+  L[0] = (L[0] < key) ? key : L[0];
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+  const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int DT>
+__device__ __forceinline__ void mfma_step(const u32x4& a, const u32x4& b, f32x16& acc) {
+  if constexpr (DT == DT_BF16) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  } else if constexpr (DT == DT_F16) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                 __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+  } else {
+    // fp32: the chunk holds k = 8g + 2m + h for m = 0..3 (storage permutation), so four
+    // k-ordered 32x32x2 steps extend one fma chain in increasing k (exact-mode contract).
+    const f32x4 af = __builtin_bit_cast(f32x4, a);
+    const f32x4 bf = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[m], bf[m], acc, 0, 0, 0);
+  }
+}
+
+// Runtime-indexed read of a register list without scratch: a select chain. The opaque copy
+// of j stops LLVM from folding the chain back into an indexed load (which would demote the
+// whole list to scratch memory).
+template <int KCAP>
+__device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) {
+  uint64_t v = L[0];
+#pragma unroll
+  for (int j = 1; j < KCAP; ++j) {
+    int jj = j;
+    asm volatile("" : "+s"(jj));
+    v = (jj == idx) ? L[j] : v;
+  }
+  return v;
+}
+
+enum { MODE_TOPK = 0, MODE_STORE = 1 };
+
+// MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
+//             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
+//             valid lower bound of its final k-th best (from the sampled pre-pass).
+// MODE_STORE: plain score tile store into score_out [n_q][score_ld] (pre-pass sample).
+template <int DT, int KCAP, int MODE>
+__global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
+    int n_rows, int n_q, int n_ktiles, int tiles_per_split, int n_row_tiles, uint32_t row_base,
+    int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init,
+    float* __restrict__ score_out, int64_t score_ld) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1;  // wave's 64-row half of the tile
+  const int wq = wave & 1;   // wave's 64-query half of the block
+  const int fr = lane & 31;
+  const int fh = lane >> 5;
+  const int split = blockIdx.x;
+  const int n_splits = gridDim.x;
+  const int q0 = blockIdx.y * kTileQ;
+  const int t_begin = split * tiles_per_split;
+  const int t_end = min(t_begin + tiles_per_split, n_row_tiles);
+
+  uint64_t* thr_key = reinterpret_cast<uint64_t*>(smem + kOffThrKey);
+  float* thr_score = reinterpret_cast<float*>(smem + kOffThrScore);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + kOffCnt);
+  int* flag = reinterpret_cast<int*>(smem + kOffFlag);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + kOffCand);
+
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  if (tid < kTileQ) {
+    // A row whose score equals the seed may still win on the row tie-break: the seed key is
+    // the smallest key with that score, minus one.
+    const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
+    thr_score[tid] = seed;
+    thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
+    cnt[tid] = 0;
+  }
+  if (tid == 0) flag[0] = 0;
+
+  // Staging map: thread t moves chunk (t & 7) of rows (t >> 3) + 32 i, i = 0..3, of both the
+  // corpus tile and the query tile: each wave instruction reads 8 full 128-B row segments.
+  const int st_row = tid >> 3;
+  const int st_ch = tid & 7;
+  const uint8_t* gB = queries + ((int64_t)q0 + st_row) * row_stride + st_ch * 16;
+  int round_id = 0;
+
+  for (int t = t_begin; t < t_end; ++t) {
+    const int64_t r0 = (int64_t)t * kTileRows;
+    const uint8_t* gA = corpus + (r0 + st_row) * row_stride + st_ch * 16;
+    u32x4 stA[4], stB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      stA[i] = *reinterpret_cast<const u32x4*>(gA + (int64_t)(32 * i) * row_stride);
+      stB[i] = *reinterpret_cast<const u32x4*>(gB + (int64_t)(32 * i) * row_stride);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = st_row + 32 * i;
+      *reinterpret_cast<u32x4*>(smem + kOffBuf0 + swz(row, st_ch)) = stA[i];
+      *reinterpret_cast<u32x4*>(smem + kOffBuf0 + kTileRows * kRowBytes + swz(row, st_ch)) = stB[i];
+    }
+    __syncthreads();
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
+
+    for (int kt = 0; kt < n_ktiles; ++kt) {
+      const bool more = kt + 1 < n_ktiles;
+      if (more) {
+        const int64_t off = (int64_t)(kt + 1) * kRowBytes;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          stA[i] = *reinterpret_cast<const u32x4*>(gA + (int64_t)(32 * i) * row_stride + off);
+          stB[i] = *reinterpret_cast<const u32x4*>(gB + (int64_t)(32 * i) * row_stride + off);
+        }
+      }
+      const unsigned char* buf = smem + ((kt & 1) ? kOffBuf1 : kOffBuf0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch = 2 * g + fh;
+        u32x4 a[2], b[2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+          a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+          b[bj] = *reinterpret_cast<const u32x4*>(buf + kTileRows * kRowBytes +
+                                                   swz(wq * 64 + bj * 32 + fr, ch));
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
+      }
+      if (more) {
+        unsigned char* nb = smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = st_row + 32 * i;
+          *reinterpret_cast<u32x4*>(nb + swz(row, st_ch)) = stA[i];
+          *reinterpret_cast<u32x4*>(nb + kTileRows * kRowBytes + swz(row, st_ch)) = stB[i];
+        }
+      }
+      __syncthreads();
+    }
+
+    if constexpr (MODE == MODE_STORE) {
+      // Score-store mode (threshold pre-pass): scores[q][row] fp32, rows of the sample only.
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        const int q = q0 + wq * 64 + bj * 32 + fr;
+        if (q < n_q) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+              const int64_t row = r0 + wr * 64 + bi * 32 + 8 * r4 + 4 * fh;
+              if (row + 3 < n_rows) {
+                f32x4 v = {acc[bi][bj][4 * r4], acc[bi][bj][4 * r4 + 1], acc[bi][bj][4 * r4 + 2],
+                           acc[bi][bj][4 * r4 + 3]};
+                *reinterpret_cast<f32x4*>(score_out + (int64_t)q * score_ld + row) = v;
+              } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (row + u < n_rows) score_out[(int64_t)q * score_ld + row + u] = acc[bi][bj][4 * r4 + u];
+              }
+            }
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+
+    // ---- epilogue: threshold filter -> LDS candidates -> owner merge (repeat on overflow).
+    // Each element test is one compare; the append path is entered only at element positions
+    // where some lane of the wave beats its query's threshold (wave-uniform branch).
+    uint64_t consumed = 0;  // accumulator elements already handed to an owner (bit e)
+    const int row_lane = (int)r0 + wr * 64 + 4 * fh;
+    for (;;) {
+      ++round_id;
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        const int ql = wq * 64 + bj * 32 + fr;
+        const float ths = (q0 + ql < n_q) ? thr_score[ql] : INFINITY;
+        const uint64_t thk = thr_key[ql];
+        float m = acc[0][bj][0];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[bi][bj][r]);
+        if (__any(m >= ths)) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int e = (bi * 2 + bj) * 16 + r;
+              const bool p = acc[bi][bj][r] >= ths && !((consumed >> e) & 1ull);
+              if (__any(p)) {
+                if (p) {
+                  // The opaque copies keep the key arithmetic inside this rarely taken branch;
+                  // hoisted, it would hold 64 keys live and spill the register file.
+                  float sv = acc[bi][bj][r];
+                  int row = row_lane + (bi * 32 + (r & 3) + 8 * (r >> 2));
+                  asm volatile("" : "+v"(sv), "+v"(row));
+                  const uint64_t key = make_key(sv, row_base + (uint32_t)row);
+                  if (row < n_rows && key > thk) {
+                    const uint32_t pos = atomicAdd(&cnt[ql], 1u);
+                    if (pos < (uint32_t)kCandCap) {
+                      cand[ql * kCandStride + pos] = key;
+                      consumed |= (1ull << e);
+                    }
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < kTileQ) {
+        const uint32_t c = cnt[tid];
+        if (c) {
+          const uint32_t n = c < (uint32_t)kCandCap ? c : (uint32_t)kCandCap;
+          for (uint32_t i = 0; i < n; ++i) list_insert<KCAP>(L, cand[tid * kCandStride + i]);
+          cnt[tid] = 0;
+          const uint64_t kth = list_at<KCAP>(L, k_out - 1);
+          if (kth > thr_key[tid]) {
+            thr_key[tid] = kth;
+            thr_score[tid] = key_score(kth);
+          }
+          if (c > (uint32_t)kCandCap) flag[0] = round_id;
+        }
+      }
+      __syncthreads();
+      if (flag[0] != round_id) break;
+    }
+  }
+
+  if (MODE == MODE_TOPK && tid < kTileQ && q0 + tid < n_q) {
+    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j)
+      if (j < k_out) dst[j] = L[j];
+  }
+}
+
+// Merge n_lists sorted key lists per query into the top k. One wave per query: every lane
+// folds a strided share into a register list, then k rounds of a wave-wide max pick winners.
+template <int KCAP>
+__global__ __launch_bounds__(64) void merge_kernel(const uint64_t* __restrict__ in, int n_lists,
+                                                   int k_in, int k, float* __restrict__ scores,
+                                                   int32_t* __restrict__ rows,
+                                                   uint64_t* __restrict__ keys_out) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t n = (int64_t)n_lists * k_in;
+  const uint64_t* src = in + (int64_t)q * n;
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  for (int64_t i = lane; i < n; i += 64) list_insert<KCAP>(L, src[i]);
+  for (int j = 0; j < k; ++j) {
+    uint64_t best = L[0];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t o = shfl_xor_u64(best, off);
+      best = o > best ? o : best;
+    }
+    if (best != 0 && L[0] == best) {
+#pragma unroll
+      for (int t = 0; t < KCAP - 1; ++t) L[t] = L[t + 1];
+      L[KCAP - 1] = 0;
+    }
+    if (lane == 0) {
+      const int64_t o = (int64_t)q * k + j;
+      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
+      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
+      if (keys_out) keys_out[o] = best;
+    }
+  }
+}
+
+// Threshold seed: k-th largest of the S sampled scores of each query (bitonic sort in LDS,
+// one 256-thread workgroup per query, S a power of two <= kSampleMax). The sample rows are
+// corpus rows, so the result is a valid lower bound of the query's final k-th best score.
+constexpr int kSampleMax = 1024;
+
+__global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict__ scores, int S,
+                                                         int k, float* __restrict__ thr) {
+  __shared__ uint32_t v[kSampleMax];
+  const int q = blockIdx.x;
+  const float* src = scores + (int64_t)q * S;
+  for (int i = threadIdx.x; i < S; i += 256) v[i] = ord_f32(src[i]);
+  __syncthreads();
+  for (int size = 2; size <= S; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < S / 2; i += 256) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const uint32_t a = v[lo], b = v[hi];
+        if ((a < b) == desc) {
+          v[lo] = b;
+          v[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) thr[q] = unord_f32(v[k - 1]);
+}
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float v) {
+  uint32_t u = __float_as_uint(v);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// fp32 storage permutation inside each group of 8: position of logical lane j.
+__device__ __forceinline__ int f32_perm(int j) { return (j & ~7) | ((j & 1) << 2) | ((j >> 1) & 3); }
+
+// fp32 rows -> storage rows (one wave per row): optional L2 normalisation, dtype conversion,
+// zero padding to d_pad, fp32 lane permutation.
+__global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restrict__ src, int64_t n,
+                                                           int dim, const int64_t* __restrict__ slots,
+                                                           int64_t start, int normalize,
+                                                           uint8_t* __restrict__ dst, int64_t row_stride,
+                                                           int d_pad, int dt) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+  if (i >= n) return;
+  const float* x = src + i * dim;
+  float nrm = 1.f;
+  if (normalize) {
+    float s = 0.f;
+    for (int j = lane; j < dim; j += 64) s = fmaf(x[j], x[j], s);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    nrm = fmaxf(sqrtf(s), 1e-12f);
+  }
+  const int64_t slot = slots ? slots[i] : start + i;
+  uint8_t* row = dst + slot * row_stride;
+  for (int j = lane; j < d_pad; j += 64) {
+    float v = j < dim ? x[j] : 0.f;
+    if (normalize) v = v / nrm;
+    if (dt == DT_BF16) {
+      reinterpret_cast<uint16_t*>(row)[j] = f32_to_bf16_rne(v);
+    } else if (dt == DT_F16) {
+      reinterpret_cast<_Float16*>(row)[j] = (_Float16)v;
+    } else {
+      reinterpret_cast<float*>(row)[f32_perm(j)] = v;
+    }
+  }
+}
+
+// Storage rows -> fp32 (inverse of convert_rows_kernel without the normalisation).
+__global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restrict__ src, int64_t start,
+                                                        int64_t n, int dim, int64_t row_stride, int dt,
+                                                        float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const uint8_t* row = src + (start + i) * row_stride;
+  for (int j = threadIdx.x & 63; j < dim; j += 64) {
+    float v;
+    if (dt == DT_BF16) {
+      v = __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(row)[j] << 16);
+    } else if (dt == DT_F16) {
+      v = (float)reinterpret_cast<const _Float16*>(row)[j];
+    } else {
+      v = reinterpret_cast<const float*>(row)[f32_perm(j)];
+    }
+    out[i * dim + j] = v;
+  }
+}
+
+}  // namespace dense
+}  // namespace ahr
+
+// =============================================================================================
+// Host side: the index handle and the C ABI.
+// =============================================================================================
+using namespace ahr;
+using namespace ahr::dense;
+
+struct ahr_index {
+  int dim = 0;
+  int dtype = 0;
+  int elem = 0;
+  int d_pad = 0;
+  int device = 0;
+  int64_t capacity = 0;
+  int64_t cap_pad = 0;
+  int64_t row_stride = 0;
+  int64_t count = 0;
+  uint8_t* rows = nullptr;
+  uint8_t* qbuf = nullptr;
+  int64_t q_cap = 0;  // rows in qbuf (multiple of 128)
+  uint64_t* part = nullptr;
+  int64_t part_cap = 0;  // uint64 elements
+  float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
+  int64_t sample_cap = 0;   // floats
+  int sample_rows = 1024;   // S; 0 disables the threshold pre-pass
+};
+
+namespace {
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int kcap_for(int k) { return k <= 8 ? 8 : (k <= 16 ? 16 : 32); }
+
+struct SearchPlan {
+  int qblocks, n_row_tiles, n_splits, tiles_per_split;
+};
+
+SearchPlan plan_search(const ahr_index* ix, int B) {
+  SearchPlan p;
+  p.qblocks = (int)cdiv(B, kTileQ);
+  p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
+  const int target_wgs = 1024;
+  int splits = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_row_tiles, cdiv(target_wgs, p.qblocks)));
+  p.tiles_per_split = std::max(1, (int)cdiv(p.n_row_tiles, splits));
+  p.n_splits = std::max(1, (int)cdiv(p.n_row_tiles, p.tiles_per_split));
+  return p;
+}
+
+int ensure_query_ws(ahr_index* ix, int B, int k) {
+  const int64_t q_need = cdiv(B, kTileQ) * kTileQ;
+  if (q_need > ix->q_cap) {
+    if (ix->qbuf) AHR_HIP(hipFree(ix->qbuf));
+    ix->qbuf = nullptr;
+    ix->q_cap = 0;
+    if (hipMalloc(&ix->qbuf, q_need * ix->row_stride) != hipSuccess)
+      return fail(AHR_ENOMEM, "query workspace allocation failed");
+    AHR_HIP(hipMemset(ix->qbuf, 0, q_need * ix->row_stride));
+    ix->q_cap = q_need;
+  }
+  // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
+  const int64_t max_tiles = std::max<int64_t>(1, ix->cap_pad / kTileRows);
+  const int64_t qblocks = cdiv(B, kTileQ);
+  const int64_t max_splits = std::min<int64_t>(max_tiles, cdiv(1024, qblocks));
+  const int64_t p_need = (int64_t)B * max_splits * k;
+  if (p_need > ix->part_cap) {
+    if (ix->part) AHR_HIP(hipFree(ix->part));
+    ix->part = nullptr;
+    ix->part_cap = 0;
+    if (hipMalloc(&ix->part, p_need * sizeof(uint64_t)) != hipSuccess)
+      return fail(AHR_ENOMEM, "partial top-k workspace allocation failed");
+    ix->part_cap = p_need;
+  }
+  const int64_t s_need = (int64_t)B * (kSampleMax + 1);
+  if (s_need > ix->sample_cap) {
+    if (ix->sample) AHR_HIP(hipFree(ix->sample));
+    ix->sample = nullptr;
+    ix->sample_cap = 0;
+    if (hipMalloc(&ix->sample, s_need * sizeof(float)) != hipSuccess)
+      return fail(AHR_ENOMEM, "sample workspace allocation failed");
+    ix->sample_cap = s_need;
+  }
+  return AHR_OK;
+}
+
+template <int DT, int KCAP, int MODE>
+void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_split,
+                 int n_row_tiles, int n_rows, int B, int k, uint32_t row_base, const float* thr,
+                 float* score_out, int64_t score_ld, hipStream_t s) {
+  static bool attr_set = false;  // > 64 KiB dynamic LDS needs the opt-in once per kernel
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tile_kernel<DT, KCAP, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    attr_set = true;
+  }
+  dim3 grid(n_splits, qblocks);
+  hipLaunchKernelGGL((topk_tile_kernel<DT, KCAP, MODE>), grid, dim3(kThreads), kLdsBytes, s,
+                     ix->rows, ix->qbuf, ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes,
+                     tiles_per_split, n_row_tiles, row_base, k, ix->part, thr, score_out, score_ld);
+}
+
+template <int DT>
+void launch_search(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base,
+                   hipStream_t s) {
+  const float* thr = nullptr;
+  const int S = ix->sample_rows;
+  if (S > 0 && ix->count >= 8 * (int64_t)S) {
+    // Threshold pre-pass: score the first S rows, take each query's k-th best.
+    float* scores = ix->sample;
+    float* t = ix->sample + (int64_t)B * S;
+    launch_tile<DT, 8, MODE_STORE>(ix, S / kTileRows, p.qblocks, 1, S / kTileRows, S, B, k, 0,
+                                   nullptr, scores, S, s);
+    hipLaunchKernelGGL(sample_kth_kernel, dim3(B), dim3(256), 0, s, scores, S, k, t);
+    thr = t;
+  }
+  const int n = (int)ix->count;
+  switch (kcap_for(k)) {
+    case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
+    case 16: launch_tile<DT, 16, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
+    default: launch_tile<DT, 32, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
+  }
+}
+
+void launch_merge(const uint64_t* in, int B, int n_lists, int k_in, int k, float* scores,
+                  int32_t* rows, uint64_t* keys_out, hipStream_t s) {
+  switch (kcap_for(k)) {
+    case 8:
+      hipLaunchKernelGGL((merge_kernel<8>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+      break;
+    case 16:
+      hipLaunchKernelGGL((merge_kernel<16>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+      break;
+    default:
+      hipLaunchKernelGGL((merge_kernel<32>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+      break;
+  }
+}
+
+int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int64_t row_base,
+              float* scores, int32_t* rows, uint64_t* keys, void* stream) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (B < 0 || k <= 0) return fail(AHR_EINVAL, "B must be >= 0 and k > 0");
+  if (k > AHR_MAX_K) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K (32)");
+  if (B == 0) return AHR_OK;
+  if (!q) return fail(AHR_EINVAL, "null query pointer");
+  if (row_base < 0 || row_base + ix->count > 0xFFFFFFFFll)
+    return fail(AHR_ERANGE, "row ids must fit in 32 bits");
+  DeviceGuard dg(ix->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int st = ensure_query_ws(ix, B, k);
+  if (st) return st;
+  hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
+                     (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
+                     ix->row_stride, ix->d_pad, ix->dtype);
+  SearchPlan p = plan_search(ix, B);
+  if (ix->count > 0) {
+    switch (ix->dtype) {
+      case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, s); break;
+      case AHR_F16: launch_search<DT_F16>(ix, p, B, k, (uint32_t)row_base, s); break;
+      default: launch_search<DT_F32>(ix, p, B, k, (uint32_t)row_base, s); break;
+    }
+  }
+  launch_merge(ix->part, B, ix->count > 0 ? p.n_splits : 0, k, k, scores, rows, keys, s);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ahr_index_create(int dim, int dtype, int64_t capacity, int device, ahr_index** out) {
+  if (!out) return fail(AHR_EINVAL, "null out pointer");
+  *out = nullptr;
+  if (dim <= 0 || capacity < 0) return fail(AHR_EINVAL, "dim must be > 0 and capacity >= 0");
+  if (dtype != AHR_F32 && dtype != AHR_F16 && dtype != AHR_BF16) return fail(AHR_EINVAL, "unknown dtype");
+  DeviceGuard dg(device);
+  ahr_index* ix = new ahr_index();
+  ix->dim = dim;
+  ix->dtype = dtype;
+  ix->elem = dtype == AHR_F32 ? 4 : 2;
+  // A k-tile is 128 B of a row: 64 half-precision or 32 fp32 lanes.
+  const int lanes_per_ktile = kRowBytes / ix->elem;
+  ix->d_pad = (int)cdiv(dim, lanes_per_ktile) * lanes_per_ktile;
+  ix->device = device;
+  ix->capacity = capacity;
+  ix->cap_pad = std::max<int64_t>(kTileRows, cdiv(capacity, kTileRows) * kTileRows);
+  ix->row_stride = (int64_t)ix->d_pad * ix->elem;
+  if (hipMalloc(&ix->rows, ix->cap_pad * ix->row_stride) != hipSuccess) {
+    delete ix;
+    return fail(AHR_ENOMEM, "corpus allocation failed");
+  }
+  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess) {
+    (void)hipFree(ix->rows);
+    delete ix;
+    return fail(AHR_EHIP, "corpus memset failed");
+  }
+  *out = ix;
+  return AHR_OK;
+}
+
+int ahr_index_destroy(ahr_index* ix) {
+  if (!ix) return AHR_OK;
+  DeviceGuard dg(ix->device);
+  if (ix->rows) (void)hipFree(ix->rows);
+  if (ix->qbuf) (void)hipFree(ix->qbuf);
+  if (ix->part) (void)hipFree(ix->part);
+  if (ix->sample) (void)hipFree(ix->sample);
+  delete ix;
+  return AHR_OK;
+}
+
+int ahr_index_upsert(ahr_index* ix, const float* vecs, int64_t n, const int64_t* slots,
+                     int64_t start_slot, int normalize, void* stream) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (n < 0) return fail(AHR_EINVAL, "n must be >= 0");
+  if (n == 0) return AHR_OK;
+  if (!vecs) return fail(AHR_EINVAL, "null vectors");
+  DeviceGuard dg(ix->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int64_t hi = start_slot + n;
+  if (slots) {
+    // Slots are device data; the caller guarantees range. We need the max for `count`:
+    // read back (synchronous on this stream) — upsert is the ingest path, not the query path.
+    int64_t* hslots = new int64_t[n];
+    hipError_t e = hipMemcpyAsync(hslots, slots, n * sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      delete[] hslots;
+      return hip_fail(e, "slot readback");
+    }
+    hi = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      if (hslots[i] < 0 || hslots[i] >= ix->capacity) {
+        delete[] hslots;
+        return fail(AHR_ERANGE, "slot out of range");
+      }
+      hi = std::max(hi, hslots[i] + 1);
+    }
+    delete[] hslots;
+  } else if (start_slot < 0 || hi > ix->capacity) {
+    return fail(AHR_ERANGE, "slot range exceeds capacity");
+  }
+  hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s, vecs, n,
+                     ix->dim, slots, start_slot, normalize, ix->rows, ix->row_stride, ix->d_pad,
+                     ix->dtype);
+  AHR_HIP(hipGetLastError());
+  ix->count = std::max(ix->count, hi);
+  return AHR_OK;
+}
+
+int ahr_index_truncate(ahr_index* ix, int64_t new_count) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (new_count < 0 || new_count > ix->capacity) return fail(AHR_ERANGE, "count out of range");
+  ix->count = new_count;
+  return AHR_OK;
+}
+
+int ahr_index_count(const ahr_index* ix, int64_t* count) {
+  if (!ix || !count) return fail(AHR_EINVAL, "null argument");
+  *count = ix->count;
+  return AHR_OK;
+}
+
+int ahr_index_info(const ahr_index* ix, int* dim, int* dtype, int64_t* capacity, int* padded_dim,
+                   int64_t* row_bytes) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (dim) *dim = ix->dim;
+  if (dtype) *dtype = ix->dtype;
+  if (capacity) *capacity = ix->capacity;
+  if (padded_dim) *padded_dim = ix->d_pad;
+  if (row_bytes) *row_bytes = ix->row_stride;
+  return AHR_OK;
+}
+
+int ahr_index_rows(const ahr_index* ix, const void** dev_rows) {
+  if (!ix || !dev_rows) return fail(AHR_EINVAL, "null argument");
+  *dev_rows = ix->rows;
+  return AHR_OK;
+}
+
+int ahr_index_read(const ahr_index* ix, int64_t start, int64_t n, float* out, void* stream) {
+  if (!ix || (n > 0 && !out)) return fail(AHR_EINVAL, "null argument");
+  if (start < 0 || n < 0 || start + n > ix->count) return fail(AHR_ERANGE, "read range outside live rows");
+  if (n == 0) return AHR_OK;
+  DeviceGuard dg(ix->device);
+  hipLaunchKernelGGL(read_rows_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), ix->rows, start, n, ix->dim,
+                     ix->row_stride, ix->dtype, out);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (max_batch <= 0 || max_k <= 0 || max_k > AHR_MAX_K) return fail(AHR_EINVAL, "bad reserve sizes");
+  DeviceGuard dg(ix->device);
+  return ensure_query_ws(ix, max_batch, max_k);
+}
+
+int ahr_index_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, float* scores,
+                    int32_t* rows, void* stream) {
+  if (!scores || !rows) return fail(AHR_EINVAL, "null output");
+  return run_query(ix, q, B, k, normalize_q, 0, scores, rows, nullptr, stream);
+}
+
+int ahr_index_query_keys(ahr_index* ix, const float* q, int B, int k, int normalize_q,
+                         int64_t row_base, uint64_t* keys, void* stream) {
+  if (!keys) return fail(AHR_EINVAL, "null output");
+  return run_query(ix, q, B, k, normalize_q, row_base, nullptr, nullptr, keys, stream);
+}
+
+int ahr_topk_merge(const uint64_t* keys_in, int B, int n_lists, int k_in, int k, float* scores,
+                   int32_t* rows, uint64_t* keys_out, void* stream) {
+  if (B < 0 || n_lists < 0 || k_in < 0 || k <= 0) return fail(AHR_EINVAL, "bad merge shape");
+  if (k > AHR_MAX_K) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K (32)");
+  if (B == 0) return AHR_OK;
+  if (!keys_in && n_lists * k_in > 0) return fail(AHR_EINVAL, "null keys");
+  launch_merge(keys_in, B, n_lists, k_in, k, scores, rows, keys_out, reinterpret_cast<hipStream_t>(stream));
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_key_decode(const uint64_t* keys, int64_t n, float* scores, int64_t* rows) {
+  if (n < 0 || (n > 0 && !keys)) return fail(AHR_EINVAL, "bad decode args");
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t k = keys[i];
+    if (scores) scores[i] = k ? key_score(k) : -INFINITY;
+    if (rows) rows[i] = k ? (int64_t)key_row(k) : -1;
+  }
+  return AHR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,369 @@
+// ahr_graph.hip — device graph (per-edge-type CSR + node attribute table) and the two graph
+// passes of the hot path, batched over queries / environments:
+//
+//   expand_rerank_kernel  HierarchicalGraph.search after the dense step
+//                         (reference src/ah_rag/graph/hierarchical_graph.py:719-782):
+//                         seeds -> 1-hop expansion (belongs_to parents / members) -> rerank ->
+//                         stable sort on the 4-decimal rounded score -> top_k.
+//   expand_kernel         GraphEnvironment.expand_{parents,children,related}
+//                         (reference src/ah_rag/agent/environment.py:393-480), incl. the 2-hop
+//                         entity -> hyperedge -> co-participant walk of expand_related.
+//
+// Both are pointer-chasing integer work bounded by a handful of neighbours per query, so one
+// thread owns one query/environment and walks its CSR rows; B queries fill the device.
+// Layout in HBM: node_type int8 [n], judge/conf/judge_term/conf_term f64 [n] (NaN = None),
+// 6 CSR lists (int64 offsets [n+1], int32 targets [nnz]) in networkx iteration order.
+#include "ahr_common.h"
+#include "ahr.h"
+
+#include <math.h>
+#include <cstring>
+#include <vector>
+
+namespace ahr {
+namespace graph {
+
+enum { ADJ_BT_OUT = 0, ADJ_BT_IN = 1, ADJ_REL_OUT = 2, ADJ_REL_IN = 3, ADJ_PI_OUT = 4, ADJ_PI_IN = 5 };
+
+struct DevGraph {
+  int64_t n_nodes;
+  const int8_t* type;
+  const double* judge;       // NaN = None
+  const double* conf;        // NaN = None
+  const double* judge_term;  // 1/(1+exp(-judge/10)) computed host-side exactly as the reference
+  const double* conf_term;   // conf/10
+  const int64_t* off[AHR_ADJ_COUNT];
+  const int32_t* tgt[AHR_ADJ_COUNT];
+};
+
+// Python's round(x, 4) for a double, exactly: the decimal rounding (half to even) of the exact
+// binary value of x, then the nearest double to that decimal (CPython float.__round__ via
+// dtoa). t = x * 10^4 is held exactly as hi + lo (TwoProduct), so the half-way test is exact.
+__device__ double py_round4(double x) {
+  if (!isfinite(x)) return x;
+  const double hi = x * 10000.0;
+  const double lo = fma(x, 10000.0, -hi);  // hi + lo == x * 10^4 exactly
+  double f = floor(hi);
+  if (hi == f && lo < 0.0) f -= 1.0;       // floor of the exact value
+  const double frac_hi = hi - f;           // exact, in [0, 1]
+  const double c = frac_hi - 0.5;          // exact when it matters (frac_hi >= 0.25)
+  double r;
+  if (frac_hi < 0.25) {
+    r = f;
+  } else if (c > -lo) {
+    r = f + 1.0;
+  } else if (c < -lo) {
+    r = f;
+  } else {
+    r = (fmod(f, 2.0) == 0.0) ? f : f + 1.0;  // exact tie: half to even
+  }
+  return r / 10000.0;
+}
+
+__device__ __forceinline__ bool has_entry(const int32_t* list, int n, int32_t v) {
+  for (int i = 0; i < n; ++i)
+    if (list[i] == v) return true;
+  return false;
+}
+
+__global__ __launch_bounds__(64) void expand_rerank_kernel(
+    DevGraph g, const int32_t* __restrict__ seed_nodes, const float* __restrict__ seed_sem, int B,
+    int k_seed, ahr_rerank_params p, int max_exp, int32_t* __restrict__ exp_nodes,
+    double* __restrict__ exp_sem, int32_t* __restrict__ exp_src, int32_t* __restrict__ exp_count,
+    int32_t* __restrict__ out_nodes, double* __restrict__ out_sem, double* __restrict__ out_score,
+    int32_t* __restrict__ out_count) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  int32_t* en = exp_nodes + (int64_t)q * max_exp;
+  double* es = exp_sem + (int64_t)q * max_exp;
+  int32_t* ex = exp_src + (int64_t)q * max_exp;
+  int n = 0;
+
+  // ---- expansion: hierarchical_graph.py:727-740 (dict insertion order; seeds overwrite in
+  // place, expansions only add absent ids)
+  for (int s = 0; s < k_seed; ++s) {
+    const int32_t nid = seed_nodes[(int64_t)q * k_seed + s];
+    if (nid < 0) continue;  // no hit (Chroma returned fewer ids)
+    const double sem = (double)seed_sem[(int64_t)q * k_seed + s];
+    int pos = -1;
+    for (int i = 0; i < n; ++i)
+      if (en[i] == nid) { pos = i; break; }
+    if (pos >= 0) {
+      es[pos] = sem;
+      ex[pos] = s;
+    } else if (n < max_exp) {
+      en[n] = nid; es[n] = sem; ex[n] = s; ++n;
+    }
+    if (nid >= g.n_nodes) continue;  // seed id unknown to the graph: no expansion
+    const int8_t t = g.type[nid];
+    int adj, lim, code;
+    double factor;
+    if (t == AHR_NODE_ENTITY) {
+      adj = ADJ_BT_OUT; lim = 2; factor = 0.9; code = -1 - AHR_NODE_SUMMARY;
+    } else if (t == AHR_NODE_SUMMARY) {
+      adj = ADJ_BT_IN; lim = p.member_top_m; factor = 0.85; code = -1 - AHR_NODE_ENTITY;
+    } else {
+      continue;
+    }
+    const int64_t b = g.off[adj][nid], e = g.off[adj][nid + 1];
+    for (int64_t j = b; j < e && j - b < lim; ++j) {
+      const int32_t v = g.tgt[adj][j];
+      if (!has_entry(en, n, v) && n < max_exp) {
+        en[n] = v; es[n] = sem * factor; ex[n] = code; ++n;
+      }
+    }
+  }
+  exp_count[q] = n;
+
+  // ---- rerank: hierarchical_graph.py:743-782, stable sort on the rounded score, [:top_k]
+  int32_t* on = out_nodes + (int64_t)q * p.top_k;
+  double* os = out_sem + (int64_t)q * p.top_k;
+  double* oc = out_score + (int64_t)q * p.top_k;
+  int m = 0;
+  for (int i = 0; i < n && p.top_k > 0; ++i) {
+    const int32_t v = en[i];
+    const bool known = v < g.n_nodes;
+    const int t = known ? g.type[v] : AHR_NODE_OTHER;
+    const double judge = known ? g.judge[v] : NAN;
+    const double conf = known ? g.conf[v] : NAN;
+    if (p.type_mask && !((p.type_mask >> t) & 1)) continue;
+    if (!isnan(p.judge_min) && (isnan(judge) || judge < p.judge_min)) continue;
+    if (!isnan(p.confidence_min) && (isnan(conf) || conf < p.confidence_min)) continue;
+    const double jt = (known && !isnan(judge)) ? g.judge_term[v] : 0.0;
+    const double ct = (known && !isnan(conf)) ? g.conf_term[v] : 0.0;
+    const double sem = es[i];
+    // left-to-right evaluation order of the reference expression (:768)
+    double score = p.alpha * sem;
+    score = score + p.beta * jt;
+    score = score + p.gamma * ct;
+    score = score + p.delta * p.layer_boost[t];
+    const double rs = py_round4(score);
+    // stable descending insertion: after every kept entry with score >= rs
+    int j = m < p.top_k ? m : p.top_k;
+    while (j > 0 && oc[j - 1] < rs) --j;
+    if (j >= p.top_k) continue;
+    const int last = (m < p.top_k ? m : p.top_k - 1);
+    for (int u = last; u > j; --u) {
+      on[u] = on[u - 1]; os[u] = os[u - 1]; oc[u] = oc[u - 1];
+    }
+    on[j] = v; os[j] = py_round4(sem); oc[j] = rs;
+    if (m < p.top_k) ++m;
+  }
+  out_count[q] = m;
+}
+
+// GraphEnvironment expansions. Streams the reference's raw neighbour sequence but keeps only
+// the first `limit` distinct ids: that prefix is all that survives dict.fromkeys()[:limit],
+// and the per-input break (raw length >= limit after an input node) is tracked on the raw count.
+struct Emit {
+  int32_t* out;
+  int limit;
+  int n;       // distinct ids kept
+  int64_t raw; // raw appends (the reference's len(expanded) before dedupe)
+  __device__ bool full() const { return n >= limit; }
+  __device__ void push(int32_t v) {
+    ++raw;
+    if (n < limit && !has_entry(out, n, v)) out[n++] = v;
+  }
+};
+
+__global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
+                                                    const int32_t* __restrict__ inputs, int B,
+                                                    int n_in, int limit, int32_t* __restrict__ out,
+                                                    int32_t* __restrict__ out_count) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  Emit em{out + (int64_t)q * limit, limit, 0, 0};
+  for (int i = 0; i < n_in && !em.full(); ++i) {
+    const int32_t nid = inputs[(int64_t)q * n_in + i];
+    if (nid < 0 || nid >= g.n_nodes) continue;  // `if nid not in self.hg.G: continue`
+    if (action == 0 || action == 1) {
+      // 0: successors with belongs_to (expand_parents :424-426)
+      // 1: predecessors with belongs_to (expand_children :401-403)
+      const int adj = action == 0 ? ADJ_BT_OUT : ADJ_BT_IN;
+      for (int64_t j = g.off[adj][nid]; j < g.off[adj][nid + 1] && !em.full(); ++j) em.push(g.tgt[adj][j]);
+    } else {
+      // expand_related :448-467
+      for (int64_t j = g.off[ADJ_REL_OUT][nid]; j < g.off[ADJ_REL_OUT][nid + 1] && !em.full(); ++j)
+        em.push(g.tgt[ADJ_REL_OUT][j]);
+      for (int64_t j = g.off[ADJ_REL_IN][nid]; j < g.off[ADJ_REL_IN][nid + 1] && !em.full(); ++j)
+        em.push(g.tgt[ADJ_REL_IN][j]);
+      if (g.type[nid] == AHR_NODE_ENTITY) {
+        for (int64_t j = g.off[ADJ_PI_OUT][nid]; j < g.off[ADJ_PI_OUT][nid + 1] && !em.full(); ++j) {
+          const int32_t h = g.tgt[ADJ_PI_OUT][j];
+          em.push(h);
+          for (int64_t u = g.off[ADJ_PI_IN][h]; u < g.off[ADJ_PI_IN][h + 1] && !em.full(); ++u) {
+            const int32_t w = g.tgt[ADJ_PI_IN][u];
+            if (w != nid) em.push(w);
+          }
+        }
+      }
+    }
+    if (em.raw >= limit) break;  // `if len(expanded) >= limit: break`
+  }
+  out_count[q] = em.n;
+}
+
+}  // namespace graph
+}  // namespace ahr
+
+using namespace ahr;
+using namespace ahr::graph;
+
+struct ahr_graph {
+  int device = 0;
+  int64_t n_nodes = 0;
+  int64_t n_edges = 0;
+  void* block = nullptr;  // one allocation holds every array
+  DevGraph dg{};
+};
+
+namespace {
+
+struct DeviceGuardG {
+  int prev = -1;
+  explicit DeviceGuardG(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuardG() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+extern "C" {
+
+int ahr_graph_create(int64_t n_nodes, const int8_t* node_type, const double* judge,
+                     const double* confidence, const double* judge_term, const double* conf_term,
+                     const int64_t* const* offsets, const int32_t* const* targets, int device,
+                     ahr_graph** out) {
+  if (!out) return fail(AHR_EINVAL, "null out pointer");
+  *out = nullptr;
+  if (n_nodes < 0 || n_nodes > 0x7FFFFFFF) return fail(AHR_EINVAL, "n_nodes out of range");
+  if (n_nodes > 0 && (!node_type || !judge || !confidence || !judge_term || !conf_term))
+    return fail(AHR_EINVAL, "null node attribute array");
+  if (!offsets || !targets) return fail(AHR_EINVAL, "null adjacency arrays");
+  int64_t nnz[AHR_ADJ_COUNT];
+  int64_t total_edges = 0;
+  for (int a = 0; a < AHR_ADJ_COUNT; ++a) {
+    if (!offsets[a]) return fail(AHR_EINVAL, "null CSR offsets");
+    nnz[a] = offsets[a][n_nodes];
+    if (nnz[a] < 0 || offsets[a][0] != 0) return fail(AHR_EINVAL, "bad CSR offsets");
+    if (nnz[a] > 0 && !targets[a]) return fail(AHR_EINVAL, "null CSR targets");
+    for (int64_t i = 0; i < nnz[a]; ++i)
+      if (targets[a][i] < 0 || targets[a][i] >= n_nodes) return fail(AHR_ERANGE, "CSR target out of range");
+    if (a % 2 == 0) total_edges += nnz[a];  // each edge appears once in an *_out list
+  }
+  // layout of the single device block
+  size_t sz = 0;
+  const size_t o_type = sz; sz = align16(sz + (size_t)n_nodes);
+  const size_t o_j = sz; sz = align16(sz + 8 * (size_t)n_nodes);
+  const size_t o_c = sz; sz = align16(sz + 8 * (size_t)n_nodes);
+  const size_t o_jt = sz; sz = align16(sz + 8 * (size_t)n_nodes);
+  const size_t o_ct = sz; sz = align16(sz + 8 * (size_t)n_nodes);
+  size_t o_off[AHR_ADJ_COUNT], o_tgt[AHR_ADJ_COUNT];
+  for (int a = 0; a < AHR_ADJ_COUNT; ++a) {
+    o_off[a] = sz; sz = align16(sz + 8 * (size_t)(n_nodes + 1));
+    o_tgt[a] = sz; sz = align16(sz + 4 * (size_t)nnz[a]);
+  }
+  std::vector<uint8_t> host(sz, 0);
+  if (n_nodes > 0) {
+    std::memcpy(host.data() + o_type, node_type, (size_t)n_nodes);
+    std::memcpy(host.data() + o_j, judge, 8 * (size_t)n_nodes);
+    std::memcpy(host.data() + o_c, confidence, 8 * (size_t)n_nodes);
+    std::memcpy(host.data() + o_jt, judge_term, 8 * (size_t)n_nodes);
+    std::memcpy(host.data() + o_ct, conf_term, 8 * (size_t)n_nodes);
+  }
+  for (int a = 0; a < AHR_ADJ_COUNT; ++a) {
+    std::memcpy(host.data() + o_off[a], offsets[a], 8 * (size_t)(n_nodes + 1));
+    if (nnz[a]) std::memcpy(host.data() + o_tgt[a], targets[a], 4 * (size_t)nnz[a]);
+  }
+  DeviceGuardG dg(device);
+  ahr_graph* g = new ahr_graph();
+  g->device = device;
+  g->n_nodes = n_nodes;
+  g->n_edges = total_edges;
+  if (hipMalloc(&g->block, sz ? sz : 16) != hipSuccess) {
+    delete g;
+    return fail(AHR_ENOMEM, "graph allocation failed");
+  }
+  if (hipMemcpy(g->block, host.data(), sz, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(g->block);
+    delete g;
+    return fail(AHR_EHIP, "graph upload failed");
+  }
+  uint8_t* base = static_cast<uint8_t*>(g->block);
+  g->dg.n_nodes = n_nodes;
+  g->dg.type = reinterpret_cast<const int8_t*>(base + o_type);
+  g->dg.judge = reinterpret_cast<const double*>(base + o_j);
+  g->dg.conf = reinterpret_cast<const double*>(base + o_c);
+  g->dg.judge_term = reinterpret_cast<const double*>(base + o_jt);
+  g->dg.conf_term = reinterpret_cast<const double*>(base + o_ct);
+  for (int a = 0; a < AHR_ADJ_COUNT; ++a) {
+    g->dg.off[a] = reinterpret_cast<const int64_t*>(base + o_off[a]);
+    g->dg.tgt[a] = reinterpret_cast<const int32_t*>(base + o_tgt[a]);
+  }
+  *out = g;
+  return AHR_OK;
+}
+
+int ahr_graph_destroy(ahr_graph* g) {
+  if (!g) return AHR_OK;
+  DeviceGuardG dg(g->device);
+  if (g->block) (void)hipFree(g->block);
+  delete g;
+  return AHR_OK;
+}
+
+int ahr_graph_info(const ahr_graph* g, int64_t* n_nodes, int64_t* n_edges) {
+  if (!g) return fail(AHR_EINVAL, "null graph");
+  if (n_nodes) *n_nodes = g->n_nodes;
+  if (n_edges) *n_edges = g->n_edges;
+  return AHR_OK;
+}
+
+int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float* seed_sem, int B,
+                            int k_seed, const ahr_rerank_params* params, int max_exp,
+                            int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
+                            int32_t* exp_count, int32_t* out_nodes, double* out_sem,
+                            double* out_score, int32_t* out_count, void* stream) {
+  if (!g || !params) return fail(AHR_EINVAL, "null graph or params");
+  if (B < 0 || k_seed < 0 || params->top_k < 0 || params->member_top_m < 0)
+    return fail(AHR_EINVAL, "negative size");
+  const int fan = params->member_top_m > 2 ? params->member_top_m : 2;
+  if (max_exp < k_seed * (1 + fan)) return fail(AHR_EINVAL, "max_exp < k_seed * (1 + max(2, member_top_m))");
+  if (B == 0) return AHR_OK;
+  if (!seed_nodes || !seed_sem || !exp_nodes || !exp_sem || !exp_src || !exp_count || !out_nodes ||
+      !out_sem || !out_score || !out_count)
+    return fail(AHR_EINVAL, "null buffer");
+  const ahr_rerank_params p = *params;
+  DeviceGuardG dg(g->device);
+  hipLaunchKernelGGL(expand_rerank_kernel, dim3((B + 63) / 64), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, seed_sem, B, k_seed,
+                     p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
+                     out_score, out_count);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int n_in, int limit,
+                     int32_t* out, int32_t* out_count, void* stream) {
+  if (!g) return fail(AHR_EINVAL, "null graph");
+  if (action < 0 || action > 2) return fail(AHR_EINVAL, "action must be 0, 1 or 2");
+  if (B < 0 || n_in < 0 || limit < 0) return fail(AHR_EINVAL, "negative size");
+  if (B == 0) return AHR_OK;
+  if ((n_in > 0 && !inputs) || !out_count || (limit > 0 && !out)) return fail(AHR_EINVAL, "null buffer");
+  DeviceGuardG dg(g->device);
+  hipLaunchKernelGGL(expand_kernel, dim3((B + 63) / 64), dim3(64), 0,
+                     reinterpret_cast<hipStream_t>(stream), g->dg, action, inputs, B, n_in, limit,
+                     out, out_count);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,184 @@
+/*
+ * ahr.h — C ABI of libahr_hip.so, the MI355X (gfx950) dense-retrieval + graph-expansion core
+ * behind AH-RAG's Python call surface.
+ *
+ * The reference (Yaron9/AH-RAG, pure Python) has no native code of its own; its hot path calls
+ * into third-party objects. Each entry point below names the reference call site it replaces:
+ *
+ *   ChromaDB collection  (un-vendored HNSW index, cosine space)
+ *     coll.upsert(ids, embeddings, ...)      src/ah_rag/graph/hierarchical_graph.py:660
+ *     coll.query(query_embeddings, n_results) src/ah_rag/graph/hierarchical_graph.py:714
+ *     client.delete_collection / reset        src/ah_rag/graph/hierarchical_graph.py:606-610
+ *   networkx neighbour scans
+ *     HierarchicalGraph._neighbors_by_edge_type     hierarchical_graph.py:441-453
+ *     search(): 1-hop expansion + rerank            hierarchical_graph.py:726-782
+ *     GraphEnvironment.expand_{children,parents,related}  src/ah_rag/agent/environment.py:393-480
+ *
+ * Conventions
+ *   - Every function returns an int status: AHR_OK (0) or a negative AHR_E* code;
+ *     ahr_last_error() returns a thread-local message for the last failure.
+ *   - Pointers documented as "device" are HIP device pointers on the handle's device.
+ *     Host pointers are only read during the call.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
+ *     All work is enqueued on it; nothing synchronises unless stated.
+ *   - Handles own their device memory. A handle is thread-compatible, not thread-safe.
+ *   - Launch functions allocate nothing once ahr_index_reserve() covered the batch,
+ *     so they may be captured into a hipGraph.
+ */
+#ifndef AHR_H_
+#define AHR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AHR_ABI_VERSION 1
+
+enum ahr_status {
+  AHR_OK = 0,
+  AHR_EINVAL = -1,   /* bad argument / shape */
+  AHR_ENOMEM = -2,   /* device allocation failed */
+  AHR_EHIP = -3,     /* HIP runtime error */
+  AHR_EUNSUP = -4,   /* unsupported parameter (e.g. k above the kernel's cap) */
+  AHR_ERANGE = -5    /* slot / node index out of range */
+};
+
+enum ahr_dtype {
+  AHR_F32 = 0,   /* exact mode: scores are a k-ordered fp32 fma chain (bit-exact vs oracle) */
+  AHR_F16 = 1,
+  AHR_BF16 = 2
+};
+
+/* Largest k the fused kernel serves (Chroma n_results). */
+#define AHR_MAX_K 32
+
+int ahr_abi_version(void);
+const char* ahr_last_error(void);
+int ahr_device_count(int* n);
+
+/* ------------------------------------------------------------------------------------------
+ * Dense index: row-major [capacity][dim] embedding matrix resident in HBM.
+ * Rows [0, count) are live. Scores are inner products of the stored rows with the queries;
+ * with L2-normalised rows and queries (normalize=1, the reference's normalize_embeddings=True)
+ * the score is the cosine similarity, i.e. 1 - Chroma's cosine distance.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct ahr_index ahr_index;
+
+/* Replaces chromadb.PersistentClient(...).get_or_create_collection("nodes", {"hnsw:space":"cosine"})
+ * (hierarchical_graph.py:605-611). */
+int ahr_index_create(int dim, int dtype, int64_t capacity, int device, ahr_index** out);
+int ahr_index_destroy(ahr_index* ix);
+
+/* Replaces coll.upsert(ids, embeddings=...) (hierarchical_graph.py:660).
+ * vecs: device fp32 [n][dim]. slots: device int64 [n] target rows, or NULL for the contiguous
+ * rows [start_slot, start_slot+n). Rows past the current count extend it; the live range must
+ * stay dense (every slot < count is written). normalize=1 L2-normalises each row first. */
+int ahr_index_upsert(ahr_index* ix, const float* vecs, int64_t n, const int64_t* slots,
+                     int64_t start_slot, int normalize, void* stream);
+
+/* Replaces client.delete_collection (hierarchical_graph.py:606-610): count := new_count. */
+int ahr_index_truncate(ahr_index* ix, int64_t new_count);
+int ahr_index_count(const ahr_index* ix, int64_t* count);
+int ahr_index_info(const ahr_index* ix, int* dim, int* dtype, int64_t* capacity,
+                   int* padded_dim, int64_t* row_bytes);
+/* Device pointer to the stored (padded, possibly permuted) rows, for tests / persistence. */
+int ahr_index_rows(const ahr_index* ix, const void** dev_rows);
+
+/* Decode stored rows [start, start+n) back to fp32 [n][dim] (device), undoing padding and the
+ * fp32 lane permutation. Used to persist the index next to the graph (SURVEY §8b on-disk). */
+int ahr_index_read(const ahr_index* ix, int64_t start, int64_t n, float* out, void* stream);
+
+/* Pre-size the per-query workspace so ahr_index_query() allocates nothing (graph-capturable). */
+int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k);
+
+/* Replaces coll.query(query_embeddings=[q], n_results=k) (hierarchical_graph.py:714), batched.
+ * q: device fp32 [B][dim]; scores: device fp32 [B][k] (descending); rows: device int32 [B][k].
+ * Ties order by row ascending. If fewer than k live rows exist the tail is (-inf, -1).
+ * normalize_q=1 L2-normalises the queries first. */
+int ahr_index_query(ahr_index* ix, const float* q, int B, int k, int normalize_q,
+                    float* scores, int32_t* rows, void* stream);
+
+/* Same search, but emits packed 64-bit sort keys (ordered score << 32 | ~row) for rows offset
+ * by row_base, so shards can all-gather and merge: keys device uint64 [B][k]. */
+int ahr_index_query_keys(ahr_index* ix, const float* q, int B, int k, int normalize_q,
+                         int64_t row_base, uint64_t* keys, void* stream);
+
+/* Merge n_lists descending key lists per query: keys_in device [B][n_lists][k_in] ->
+ * top k as scores/rows (and optionally keys_out [B][k]). Used for the cross-shard merge
+ * after the RCCL all-gather. */
+int ahr_topk_merge(const uint64_t* keys_in, int B, int n_lists, int k_in, int k,
+                   float* scores, int32_t* rows, uint64_t* keys_out, void* stream);
+
+/* Decode keys -> (score, row); host-side helper mirrors the device format. */
+int ahr_key_decode(const uint64_t* keys, int64_t n, float* scores, int64_t* rows);
+
+/* ------------------------------------------------------------------------------------------
+ * Graph: per-edge-type CSR adjacency + node attribute table resident in HBM.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct ahr_graph ahr_graph;
+
+enum ahr_node_type { AHR_NODE_OTHER = 0, AHR_NODE_ENTITY = 1, AHR_NODE_SUMMARY = 2,
+                     AHR_NODE_HYPEREDGE = 3 };
+
+/* Adjacency lists, each a CSR (offsets [n_nodes+1], targets [nnz]) in the order networkx
+ * iterates neighbours of the live graph (G._succ / G._pred; for a graph that went through
+ * save/load that is the order of hierarchical_graph.py:191-202):
+ *   0 belongs_to out   (entity -> summaries, get_belongs_to)
+ *   1 belongs_to in    (summary <- members, get_summary_members)
+ *   2 related_to out   3 related_to in
+ *   4 participates_in out (entity -> hyperedges)   5 participates_in in (hyperedge <- entities)
+ * All arrays are host pointers and are copied to the device.
+ * judge / confidence: NaN encodes Python None. judge_term / conf_term are the rerank terms
+ * 1/(1+exp(-(judge/10))) and conf/10 (hierarchical_graph.py:766-767), computed by the caller with
+ * the reference's own float64 arithmetic so the device score matches bit for bit. */
+#define AHR_ADJ_COUNT 6
+int ahr_graph_create(int64_t n_nodes, const int8_t* node_type, const double* judge,
+                     const double* confidence, const double* judge_term, const double* conf_term,
+                     const int64_t* const* offsets, const int32_t* const* targets, int device,
+                     ahr_graph** out);
+int ahr_graph_destroy(ahr_graph* g);
+
+/* Search parameters, hierarchical_graph.py:682-699. */
+typedef struct ahr_rerank_params {
+  double alpha, beta, gamma, delta;
+  double judge_min;       /* NaN = no filter */
+  double confidence_min;  /* NaN = no filter */
+  double layer_boost[4];  /* indexed by ahr_node_type */
+  int type_mask;          /* bit t set = node type t allowed; 0 = no filter */
+  int member_top_m;
+  int top_k;
+} ahr_rerank_params;
+
+/* Batched search() tail: seeds -> 1-hop expansion -> rerank (hierarchical_graph.py:726-782).
+ * seed_nodes: device int32 [B][k_seed] (-1 = absent; >= n_nodes = id unknown to the graph);
+ * seed_sem: device fp32 [B][k_seed] (semantic = 1 - cosine distance).
+ * Outputs (device, per query q):
+ *   exp_nodes/exp_sem/exp_src [B][max_exp], exp_count [B]: the `expanded` dict in insertion
+ *     order; exp_src = seed index (entry owned by a seed) or -1 - assumed_node_type (added by
+ *     expansion with meta {"expanded": True});
+ *   out_nodes/out_sem/out_score [B][top_k], out_count [B]: `reranked`, with out_sem and
+ *     out_score rounded to 4 decimals exactly like Python round(x, 4), stable-sorted on the
+ *     rounded score.
+ * max_exp must be >= k_seed * (1 + max(2, member_top_m)). */
+int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float* seed_sem,
+                            int B, int k_seed, const ahr_rerank_params* params, int max_exp,
+                            int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
+                            int32_t* exp_count, int32_t* out_nodes, double* out_sem,
+                            double* out_score, int32_t* out_count, void* stream);
+
+/* Batched environment expansions (environment.py:393-480).
+ * action: 0 expand_parents, 1 expand_children, 2 expand_related.
+ * inputs: device int32 [B][n_in] (-1 = absent / not in graph); out: device int32 [B][limit],
+ * out_count [B]. Reproduces the reference's per-input early break (>= limit after an input
+ * node's neighbours were appended), first-occurrence dedupe and truncation to limit. */
+int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int n_in,
+                     int limit, int32_t* out, int32_t* out_count, void* stream);
+
+int ahr_graph_info(const ahr_graph* g, int64_t* n_nodes, int64_t* n_edges);
+
+#ifdef __cplusplus
+}
+#endif
+#endif  /* AHR_H_ */

@@ -1,0 +1,24 @@
+"""Build the C oracle (test infrastructure): oracle/_build/libahr_oracle.so."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT_DIR = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT_DIR, "libahr_oracle.so")
+SRC = os.path.join(HERE, "ahr_oracle.c")
+
+
+def build(force: bool = False) -> str:
+    os.makedirs(OUT_DIR, exist_ok=True)
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+        return LIB
+    cmd = ["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fopenmp", "-shared", "-fPIC",
+           SRC, "-o", LIB, "-lm"]
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True))
