@@ -193,6 +193,32 @@ class DenseIndex:
                       "ahr_index_read")
         return out
 
+    # -- diagnostics --------------------------------------------------------------------------
+    def set_sample_rows(self, rows: int) -> None:
+        """Rows scored by the threshold pre-pass (0 disables it)."""
+        nat.check(nat.lib().ahr_index_set_sample_rows(self._h, int(rows)), "ahr_index_set_sample_rows")
+
+    def plan(self, batch: int) -> dict:
+        a, b, c = nat.ctypes.c_int(), nat.ctypes.c_int(), nat.ctypes.c_int()
+        nat.check(nat.lib().ahr_index_plan(self._h, int(batch), nat.ctypes.byref(a), nat.ctypes.byref(b),
+                                           nat.ctypes.byref(c)), "ahr_index_plan")
+        return {"n_splits": a.value, "tiles_per_split": b.value, "qblocks": c.value}
+
+    def profile_begin(self, max_calls: int) -> None:
+        """Record HIP events around each query stage for the next max_calls calls."""
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_profile_begin(self._h, int(max_calls)), "ahr_index_profile_begin")
+
+    STAGES = ("convert", "threshold_prepass", "tile_topk", "merge")
+
+    def profile_end(self) -> dict:
+        """Per-stage summed milliseconds and the number of recorded calls."""
+        arr = (nat.ctypes.c_float * 4)()
+        n = nat.ctypes.c_int()
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_profile_end(self._h, arr, nat.ctypes.byref(n)), "ahr_index_profile_end")
+        return {"calls": n.value, "ms_sum": {name: float(arr[i]) for i, name in enumerate(self.STAGES)}}
+
     # -- reads (hierarchical_graph.py:714) -----------------------------------------------------
     def query(self, queries: ArrayLike, k: int, normalize: bool = False,
               stream: Optional[torch.cuda.Stream] = None,

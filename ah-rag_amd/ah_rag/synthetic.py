@@ -1,0 +1,96 @@
+"""Synthetic HotpotQA-shaped corpora: no dataset or encoder weights are
+reachable offline, so the benchmark corpora are generated with a fixed seed.
+
+C2  N = 90,000 rows = 87,000 entity + 3,000 summary, d = 768:
+    entity row  = normalize(c[topic] + 0.35 * eps), eps ~ N(0, I/d), 3,000 unit centroids;
+    summary row = normalize(mean of its member entity rows) (semantic_aggregator.py:194 analogue).
+C3  N = 5,000,000 rows, same generator with 50,000 centroids, generated in chunks on the GPU.
+Queries: half perturbed corpus rows normalize(x_r + 0.2 eps) (known source row), half fresh
+cluster draws normalize(c[t] + 0.35 eps).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Iterator, Optional, Tuple
+
+import numpy as np
+import torch
+
+SEED = 20251003
+
+
+def _normalize(x: torch.Tensor) -> torch.Tensor:
+    return x / x.norm(dim=1, keepdim=True).clamp_min(1e-12)
+
+
+@dataclass
+class CorpusSpec:
+    n_entities: int = 87_000
+    n_summaries: int = 3_000
+    dim: int = 768
+    n_centroids: int = 3_000
+    noise: float = 0.35
+    seed: int = SEED
+
+    @property
+    def n_rows(self) -> int:
+        return self.n_entities + self.n_summaries
+
+
+HOTPOT_90K = CorpusSpec()
+SYNTH_5M = CorpusSpec(n_entities=5_000_000, n_summaries=0, n_centroids=50_000)
+
+
+class SyntheticCorpus:
+    """Deterministic corpus: rows are produced chunk by chunk on `device` (torch Generator)."""
+
+    def __init__(self, spec: CorpusSpec = HOTPOT_90K, device: Optional[torch.device] = None) -> None:
+        self.spec = spec
+        self.device = device or torch.device("cpu")
+        g = torch.Generator(device="cpu").manual_seed(spec.seed)
+        self.centroids = _normalize(torch.randn(spec.n_centroids, spec.dim, generator=g)).to(self.device)
+        self.topics = torch.randint(0, spec.n_centroids, (spec.n_entities,), generator=g)
+
+    def entity_chunks(self, chunk: int = 100_000) -> Iterator[Tuple[int, torch.Tensor]]:
+        s = self.spec
+        for start in range(0, s.n_entities, chunk):
+            n = min(chunk, s.n_entities - start)
+            g = torch.Generator(device=self.device).manual_seed(s.seed + 1 + start // chunk)
+            eps = torch.randn(n, s.dim, generator=g, device=self.device) / np.sqrt(s.dim)
+            t = self.topics[start:start + n].to(self.device)
+            yield start, _normalize(self.centroids[t] + s.noise * eps)
+
+    def rows(self) -> torch.Tensor:
+        """All rows [n_rows, dim] fp32 on `device` (entities first, then summaries)."""
+        s = self.spec
+        out = torch.empty(s.n_rows, s.dim, dtype=torch.float32, device=self.device)
+        for start, x in self.entity_chunks():
+            out[start:start + x.shape[0]] = x
+        if s.n_summaries:
+            ent = out[:s.n_entities]
+            topic = self.topics.to(self.device)
+            # summaries = normalized member means over the first n_summaries topics
+            sums = torch.zeros(s.n_centroids, s.dim, device=self.device)
+            sums.index_add_(0, topic, ent)
+            out[s.n_entities:] = _normalize(sums[:s.n_summaries] + 1e-6 * self.centroids[:s.n_summaries])
+        return out
+
+    def queries(self, batch: int, rows: Optional[torch.Tensor] = None, salt: int = 0
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(queries fp32 [batch, dim], source_row int64 [batch] or -1 for fresh draws)."""
+        s = self.spec
+        g = torch.Generator(device="cpu").manual_seed(s.seed + 7919 * (salt + 1))
+        half = batch // 2
+        n_rows = s.n_rows
+        src = torch.randint(0, n_rows, (half,), generator=g)
+        t = torch.randint(0, s.n_centroids, (batch - half,), generator=g)
+        eps = torch.randn(batch, s.dim, generator=g) / np.sqrt(s.dim)
+        eps = eps.to(self.device)
+        if rows is None:
+            rows = self.rows()
+        base = torch.cat([rows[src.to(rows.device)].to(self.device),
+                          self.centroids[t.to(self.device)]])
+        scale = torch.cat([torch.full((half, 1), 0.2), torch.full((batch - half, 1), s.noise)]).to(self.device)
+        q = _normalize(base + scale * eps)
+        source = torch.cat([src, torch.full((batch - half,), -1, dtype=torch.int64)])
+        return q, source

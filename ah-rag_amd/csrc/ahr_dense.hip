@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <math.h>
+#include <vector>
 
 namespace ahr {
 namespace dense {
@@ -491,6 +492,11 @@ struct ahr_index {
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
   int64_t sample_cap = 0;   // floats
   int sample_rows = 1024;   // S; 0 disables the threshold pre-pass
+  // Optional stage timing: a ring of HIP events, kStages+1 per query call, recorded on the
+  // call's stream (ahr_index_profile_begin / _end).
+  std::vector<hipEvent_t> prof_events;
+  int prof_max_calls = 0;
+  int prof_calls = 0;
 };
 
 namespace {
@@ -510,6 +516,13 @@ struct DeviceGuard {
 };
 
 int kcap_for(int k) { return k <= 8 ? 8 : (k <= 16 ? 16 : 32); }
+
+constexpr int kStages = 4;  // convert, threshold pre-pass, tile kernel, merge
+
+inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
+  if (ix->prof_calls < ix->prof_max_calls)
+    (void)hipEventRecord(ix->prof_events[(size_t)ix->prof_calls * (kStages + 1) + stage], s);
+}
 
 struct SearchPlan {
   int qblocks, n_row_tiles, n_splits, tiles_per_split;
@@ -579,9 +592,10 @@ void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_s
 }
 
 template <int DT>
-void launch_search(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base,
+void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base,
                    hipStream_t s) {
   const float* thr = nullptr;
+  prof_mark(ix, 1, s);
   const int S = ix->sample_rows;
   if (S > 0 && ix->count >= 8 * (int64_t)S) {
     // Threshold pre-pass: score the first S rows, take each query's k-th best.
@@ -592,6 +606,7 @@ void launch_search(const ahr_index* ix, const SearchPlan& p, int B, int k, uint3
     hipLaunchKernelGGL(sample_kth_kernel, dim3(B), dim3(256), 0, s, scores, S, k, t);
     thr = t;
   }
+  prof_mark(ix, 2, s);
   const int n = (int)ix->count;
   switch (kcap_for(k)) {
     case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
@@ -628,6 +643,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int st = ensure_query_ws(ix, B, k);
   if (st) return st;
+  prof_mark(ix, 0, s);
   hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
                      (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                      ix->row_stride, ix->d_pad, ix->dtype);
@@ -638,8 +654,14 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
       case AHR_F16: launch_search<DT_F16>(ix, p, B, k, (uint32_t)row_base, s); break;
       default: launch_search<DT_F32>(ix, p, B, k, (uint32_t)row_base, s); break;
     }
+  } else {
+    prof_mark(ix, 1, s);
+    prof_mark(ix, 2, s);
   }
+  prof_mark(ix, 3, s);
   launch_merge(ix->part, B, ix->count > 0 ? p.n_splits : 0, k, k, scores, rows, keys, s);
+  prof_mark(ix, 4, s);
+  if (ix->prof_calls < ix->prof_max_calls) ++ix->prof_calls;
   AHR_HIP(hipGetLastError());
   return AHR_OK;
 }
@@ -685,6 +707,7 @@ int ahr_index_destroy(ahr_index* ix) {
   if (ix->qbuf) (void)hipFree(ix->qbuf);
   if (ix->part) (void)hipFree(ix->part);
   if (ix->sample) (void)hipFree(ix->sample);
+  for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
   delete ix;
   return AHR_OK;
 }
@@ -767,6 +790,58 @@ int ahr_index_read(const ahr_index* ix, int64_t start, int64_t n, float* out, vo
                      reinterpret_cast<hipStream_t>(stream), ix->rows, start, n, ix->dim,
                      ix->row_stride, ix->dtype, out);
   AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_index_profile_begin(ahr_index* ix, int max_calls) {
+  if (!ix || max_calls < 0) return fail(AHR_EINVAL, "bad profile request");
+  DeviceGuard dg(ix->device);
+  for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
+  ix->prof_events.clear();
+  ix->prof_events.resize((size_t)max_calls * (kStages + 1));
+  for (auto& e : ix->prof_events) AHR_HIP(hipEventCreate(&e));
+  ix->prof_max_calls = max_calls;
+  ix->prof_calls = 0;
+  return AHR_OK;
+}
+
+int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum, int* n_calls) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  DeviceGuard dg(ix->device);
+  float sum[kStages] = {0, 0, 0, 0};
+  for (int c = 0; c < ix->prof_calls; ++c) {
+    hipEvent_t* ev = &ix->prof_events[(size_t)c * (kStages + 1)];
+    AHR_HIP(hipEventSynchronize(ev[kStages]));
+    for (int st = 0; st < kStages; ++st) {
+      float ms = 0.f;
+      AHR_HIP(hipEventElapsedTime(&ms, ev[st], ev[st + 1]));
+      sum[st] += ms;
+    }
+  }
+  if (stage_ms_sum)
+    for (int st = 0; st < kStages; ++st) stage_ms_sum[st] = sum[st];
+  if (n_calls) *n_calls = ix->prof_calls;
+  for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
+  ix->prof_events.clear();
+  ix->prof_max_calls = 0;
+  ix->prof_calls = 0;
+  return AHR_OK;
+}
+
+int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (rows < 0 || rows > kSampleMax || (rows & (rows - 1)) || (rows && rows < kTileRows))
+    return fail(AHR_EINVAL, "sample rows must be 0 or a power of two in [128, 1024]");
+  ix->sample_rows = rows;
+  return AHR_OK;
+}
+
+int ahr_index_plan(const ahr_index* ix, int B, int* n_splits, int* tiles_per_split, int* qblocks) {
+  if (!ix || B <= 0) return fail(AHR_EINVAL, "bad plan request");
+  SearchPlan p = plan_search(ix, B);
+  if (n_splits) *n_splits = p.n_splits;
+  if (tiles_per_split) *tiles_per_split = p.tiles_per_split;
+  if (qblocks) *qblocks = p.qblocks;
   return AHR_OK;
 }
 

@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X dense-retrieval hot path.
+
+Metric (BASELINE.json): queries/sec + recall@10, d=768 HotpotQA corpus, 1/2/4/8 MI355X.
+Workload (default, BASELINE.json configs[1]): HotpotQA-distractor-shaped graph corpus,
+90,000 rows (87k entity + 3k summary) x d=768 stored bf16 in HBM, batch of 1,024 queries,
+exact top-10 by inner product of L2-normalised vectors (= cosine), fused Q.N^T + top-k kernel.
+One step = one batch through ahr_index_query (query conversion, threshold pre-pass, fused tile
+kernel, cross-split merge). Inputs are resident in HBM before the timed region.
+
+--workload synth5m runs configs[2] (5M x 768 fp16). --gpus N (launched by torch.distributed.run)
+runs one process per GPU: --shard queries (default) gives every rank a corpus replica and its own
+query batch (weak scaling, no collective on the data path); --shard rows splits the corpus rows
+across ranks and merges the per-rank top-k with an RCCL all-gather (strong scaling, configs[3]).
+
+The data is synthetic (no dataset or encoder weights offline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "ah-rag_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from ah_rag.embeddings import DenseIndex, merge_topk_keys  # noqa: E402
+from ah_rag.synthetic import HOTPOT_90K, SYNTH_5M, SyntheticCorpus  # noqa: E402
+
+METRIC = "queries/sec + recall@10, d=768 HotpotQA corpus, 1/2/4/8 MI355X"
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f16": 2500.0, "f32": 157.3}  # MI355X_MICROARCH.md, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=["hotpot90k", "synth5m"], default="hotpot90k")
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--dtype", choices=["bf16", "f16", "f32"], default=None)
+    ap.add_argument("--shard", choices=["queries", "rows"], default="queries")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (s)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--recall-queries", type=int, default=256)
+    return ap.parse_args()
+
+
+def recall_at_k(got: np.ndarray, exact: np.ndarray) -> float:
+    k = exact.shape[1]
+    hits = [len(set(g.tolist()) & set(e.tolist())) for g, e in zip(got, exact)]
+    return float(np.mean(hits) / k)
+
+
+def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float) -> dict:
+    """The reference math on the host: fp32 BLAS Q @ C.T + argpartition top-k (oracle port)."""
+    from oracle import dense_ref  # checker / baseline only
+
+    try:
+        from threadpoolctl import threadpool_info
+        blas = [i for i in threadpool_info() if i.get("user_api") == "blas"]
+        threads = int(blas[0]["num_threads"]) if blas else 1
+        blas_name = f"{blas[0].get('internal_api')} {blas[0].get('version')}" if blas else "unknown"
+    except Exception:
+        threads, blas_name = int(os.environ.get("OMP_NUM_THREADS", "1")), "unknown"
+    chunk = 256
+    done, t0 = 0, time.perf_counter()
+    i = 0
+    while True:
+        qs = queries[(i * chunk) % len(queries):][:chunk]
+        dense_ref.topk_numpy(rows, qs, k)
+        done += len(qs)
+        i += 1
+        if time.perf_counter() - t0 >= budget_s and done >= chunk:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 2), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": (f"{done} queries in {chunk}-query batches over the full {rows.shape[0]}x{rows.shape[1]} "
+                       f"fp32 corpus, numpy BLAS ({blas_name}, {threads} threads) + argpartition top-{k}; "
+                       f"{dt:.1f}s; host os.cpu_count()={os.cpu_count()}")}
+
+
+def read_traffic(kernel: str, launches_per_step: int = 1):
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        return data.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main() -> None:
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    spec = HOTPOT_90K if args.workload == "hotpot90k" else SYNTH_5M
+    dtype = args.dtype or ("bf16" if args.workload == "hotpot90k" else "f16")
+    B, k = args.batch, args.k
+    corpus = SyntheticCorpus(spec, dev)
+    rows = corpus.rows()
+    N, d = rows.shape
+    if args.shard == "rows" and world > 1:
+        bounds = np.linspace(0, N, world + 1).astype(np.int64)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    else:
+        lo, hi = 0, N
+    index = DenseIndex(d, hi - lo, dtype=dtype, device=dev)
+    for s in range(lo, hi, 1_000_000):
+        index.upsert(rows[s:min(hi, s + 1_000_000)], start=s - lo)
+    salt = rank if args.shard == "queries" else 0
+    q, src = corpus.queries(B, rows, salt=salt)
+    index.reserve(B, k)
+    scores = torch.empty((B, k), dtype=torch.float32, device=dev)
+    out_rows = torch.empty((B, k), dtype=torch.int32, device=dev)
+    keys = torch.empty((B, k), dtype=torch.int64, device=dev)
+    gathered = torch.empty((world, B, k), dtype=torch.int64, device=dev) if world > 1 else None
+    sharded = args.shard == "rows" and world > 1
+
+    def step():
+        if sharded:
+            index.query_keys(q, k, row_base=lo, out=keys)
+            dist.all_gather_into_tensor(gathered, keys)
+            s_, r_, _ = merge_topk_keys(gathered.permute(1, 0, 2), k)
+            return s_, r_
+        index.query(q, k, out=(scores, out_rows))
+        return scores, out_rows
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    index.profile_begin(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    prof = index.profile_end()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    q_per_step = B * world if not sharded else B
+    value = q_per_step * args.steps / dt
+
+    # ---- recall@10 against exact fp32 ground truth of the fp32 source vectors (untimed)
+    got_rows = res[1].cpu().numpy().astype(np.int64)
+    nq = min(args.recall_queries, B)
+    if N <= 200_000:
+        from oracle import dense_ref
+        _, exact = dense_ref.topk_numpy(rows.cpu().numpy(), q[:nq].cpu().numpy(), k)
+    else:
+        gt = DenseIndex(d, N, dtype="f32", device=dev)
+        for s in range(0, N, 1_000_000):
+            gt.upsert(rows[s:s + 1_000_000], start=s)
+        exact = gt.query(q[:nq], k)[1].cpu().numpy().astype(np.int64)
+        gt.close()
+    if sharded:
+        got_global = got_rows[:nq]
+    else:
+        got_global = got_rows[:nq] + lo
+    rec = recall_at_k(got_global, exact)
+
+    if rank == 0:
+        calls = max(1, prof["calls"])
+        tile_ms = prof["ms_sum"]["tile_topk"] / calls
+        n_local = hi - lo
+        flops = 2.0 * B * n_local * d
+        achieved_tf = flops / (tile_ms * 1e-3) / 1e12
+        peak = MFMA_PEAK_TFLOPS[dtype]
+        elem = 4 if dtype == "f32" else 2
+        alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
+        plan = index.plan(B)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if not sharded else "strong",
+            "vs_baseline": None,
+            "dtype": dtype,
+            "data": "synthetic (SURVEY.md §8d clustered generator, seed 20251003; no HotpotQA/encoder offline)",
+            "recall_at_10": round(rec, 4),
+            "config": {
+                "workload": ("hotpot90k: HotpotQA-distractor-shaped corpus 87k entity + 3k summary rows"
+                             if args.workload == "hotpot90k" else "synth5m: 5M-row synthetic corpus"),
+                "corpus_rows": N, "dim": d, "batch": B, "top_k": k, "index_dtype": dtype,
+                "parallelism": (f"rows{world}" if sharded else (f"queries{world}" if world > 1 else "single")),
+                "launch": plan,
+            },
+            "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
+            "roofline": {
+                "kernel": "topk_tile_kernel (fused MFMA Q.N^T + top-k)",
+                "bound": "mfma",
+                "achieved": round(achieved_tf, 2),
+                "peak": peak,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tf / peak, 4),
+                "traffic": read_traffic("topk_tile_kernel"),
+                "algorithmic_flops_per_launch": flops,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "hbm_equiv_GBs": round(alg_bytes / (tile_ms * 1e-3) / 1e9, 1),
+                "avg_launch_ms": round(tile_ms, 5),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            nc = min(len(q), 1024)
+            out["cpu_baseline"] = cpu_baseline(rows.cpu().numpy(), q[:nc].cpu().numpy(), k, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    index.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

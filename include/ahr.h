@@ -90,6 +90,18 @@ int ahr_index_rows(const ahr_index* ix, const void** dev_rows);
  * fp32 lane permutation. Used to persist the index next to the graph (SURVEY §8b on-disk). */
 int ahr_index_read(const ahr_index* ix, int64_t start, int64_t n, float* out, void* stream);
 
+/* Stage timing with HIP events recorded on each query call's stream. Stages:
+ * 0 query conversion, 1 threshold pre-pass, 2 fused tile kernel, 3 cross-split merge.
+ * begin: arm for up to max_calls calls; end: wait, return per-stage sums (ms) and the call count. */
+int ahr_index_profile_begin(ahr_index* ix, int max_calls);
+int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_calls);
+
+/* Rows scored by the threshold pre-pass (0 disables it; else a power of two in [128, 1024]). */
+int ahr_index_set_sample_rows(ahr_index* ix, int rows);
+
+/* Launch geometry the next query of batch B would use (diagnostics / bench reporting). */
+int ahr_index_plan(const ahr_index* ix, int B, int* n_splits, int* tiles_per_split, int* qblocks);
+
 /* Pre-size the per-query workspace so ahr_index_query() allocates nothing (graph-capturable). */
 int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k);
 
