@@ -198,6 +198,10 @@ class DenseIndex:
         """Rows scored by the threshold pre-pass (0 disables it)."""
         nat.check(nat.lib().ahr_index_set_sample_rows(self._h, int(rows)), "ahr_index_set_sample_rows")
 
+    def set_debug_flags(self, flags: int) -> None:
+        """Ablation switches (2 = skip the top-k epilogue; results become garbage)."""
+        nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
+
     def plan(self, batch: int) -> dict:
         a, b, c = nat.ctypes.c_int(), nat.ctypes.c_int(), nat.ctypes.c_int()
         nat.check(nat.lib().ahr_index_plan(self._h, int(batch), nat.ctypes.byref(a), nat.ctypes.byref(b),

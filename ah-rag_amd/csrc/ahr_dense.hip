@@ -44,21 +44,22 @@ constexpr int kTileRows = 128;
 constexpr int kTileQ = 128;
 constexpr int kRowBytes = 128;  // one k-tile of one row: 8 chunks of 16 B
 constexpr int kBufBytes = (kTileRows + kTileQ) * kRowBytes;  // 32 KiB: A tile, then B tile
-constexpr int kCandCap = 32;
-constexpr int kCandStride = kCandCap + 1;  // odd u64 stride: owners hit distinct banks
+constexpr int kProdCap = 8;  // candidate slots per (query, producer lane); 4 producers per query
 
 // LDS map (bytes). The candidate lists overlay the two staging buffers: they are only live
 // between the last k-tile of a corpus tile and the first k-tile of the next one.
 constexpr int kOffBuf0 = 0;
 constexpr int kOffBuf1 = kBufBytes;
 constexpr int kOffCand = 0;
-constexpr int kCandBytes = kTileQ * kCandStride * 8;
+constexpr int kCandBytes = kTileQ * 4 * kProdCap * 8;   // 32 KiB
+constexpr int kOffScratch = kOffCand + kCandBytes;         // 4 waves x 64 lanes x 32 floats
+constexpr int kScratchBytes = 4 * 64 * 32 * 4;             // 32 KiB
 constexpr int kOffThrKey = 2 * kBufBytes;
 constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
 constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
-constexpr int kOffFlag = kOffCnt + kTileQ * 4;
+constexpr int kOffFlag = kOffCnt + kTileQ * 4 * 4;
 constexpr int kLdsBytes = kOffFlag + 16;
-static_assert(kCandBytes <= 2 * kBufBytes, "candidate overlay must fit the staging buffers");
+static_assert(kCandBytes + kScratchBytes <= 2 * kBufBytes, "epilogue overlay must fit the staging buffers");
 static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
 
 // XOR swizzle of 16-B chunks inside a 128-B row: a ds_read_b128 lane group (rows
@@ -78,6 +79,29 @@ __device__ __forceinline__ void list_insert(uint64_t (&L)[KCAP], uint64_t key) {
     L[j] = (prev < key) ? prev : ((L[j] < key) ? key : L[j]);
   }
   L[0] = (L[0] < key) ? key : L[0];
+}
+
+// Wave64 max of packed keys with DPP row shifts + row broadcasts (gfx9 family): no LDS
+// round trips, unlike __shfl_xor (ds_bpermute). Returns the max in every lane.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROW_MASK, 0xf, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ uint64_t max_u64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+  x = max_u64(x, dpp_u64<0x111, 0xf>(x));  // row_shr:1
+  x = max_u64(x, dpp_u64<0x112, 0xf>(x));  // row_shr:2
+  x = max_u64(x, dpp_u64<0x114, 0xf>(x));  // row_shr:4
+  x = max_u64(x, dpp_u64<0x118, 0xf>(x));  // row_shr:8  -> lane 15 of each row: row max
+  x = max_u64(x, dpp_u64<0x142, 0xa>(x));  // row_bcast:15 -> lane 31, 63: max of row pairs
+  x = max_u64(x, dpp_u64<0x143, 0xc>(x));  // row_bcast:31 -> lane 63: wave max
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
@@ -119,18 +143,19 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) 
   return v;
 }
 
-enum { MODE_TOPK = 0, MODE_STORE = 1 };
+enum { MODE_TOPK = 0, MODE_GROUPMAX = 1 };
+enum { kFlagXcdRemap = 1, kFlagSkipEpilogue = 2 };  // kFlagSkipEpilogue: ablation only (wrong output)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
 //             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
 //             valid lower bound of its final k-th best (from the sampled pre-pass).
-// MODE_STORE: plain score tile store into score_out [n_q][score_ld] (pre-pass sample).
+// MODE_GROUPMAX: 16-row group maxima of the scores into score_out [n_q][score_ld] (pre-pass).
 template <int DT, int KCAP, int MODE>
 __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
     int n_rows, int n_q, int n_ktiles, int tiles_per_split, int n_row_tiles, uint32_t row_base,
     int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init,
-    float* __restrict__ score_out, int64_t score_ld) {
+    float* __restrict__ score_out, int64_t score_ld, int n_splits, int qblocks, int flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -139,9 +164,21 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
   const int wq = wave & 1;   // wave's 64-query half of the block
   const int fr = lane & 31;
   const int fh = lane >> 5;
-  const int split = blockIdx.x;
-  const int n_splits = gridDim.x;
-  const int q0 = blockIdx.y * kTileQ;
+  // 1-D grid. With kFlagXcdRemap, the qblocks workgroups that stream the same corpus rows
+  // (one split) get ids that are equal mod 8 and adjacent in dispatch order: the dispatcher
+  // deals ids round-robin over the 8 XCDs, so they share one L2 and read each corpus tile from
+  // HBM once (placement is a speed hint only; any placement gives the same result).
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q0 = qb * kTileQ;
   const int t_begin = split * tiles_per_split;
   const int t_end = min(t_begin + tiles_per_split, n_row_tiles);
 
@@ -160,9 +197,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
     const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
     thr_score[tid] = seed;
     thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
-    cnt[tid] = 0;
   }
-  if (tid == 0) flag[0] = 0;
+  if (tid < 2) flag[tid] = 0;
 
   // Staging map: thread t moves chunk (t & 7) of rows (t >> 3) + 32 i, i = 0..3, of both the
   // corpus tile and the query tile: each wave instruction reads 8 full 128-B row segments.
@@ -235,38 +271,47 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
       __syncthreads();
     }
 
-    if constexpr (MODE == MODE_STORE) {
-      // Score-store mode (threshold pre-pass): scores[q][row] fp32, rows of the sample only.
+    if constexpr (MODE == MODE_GROUPMAX) {
+      // Threshold pre-pass: per query, the max of each 16-row group (one lane's 16 registers of
+      // one 32x32 block). The k-th largest group max is a valid lower bound of the k-th best
+      // score: each group max is a distinct corpus row.
 #pragma unroll
       for (int bj = 0; bj < 2; ++bj) {
         const int q = q0 + wq * 64 + bj * 32 + fr;
-        if (q < n_q) {
 #pragma unroll
-          for (int bi = 0; bi < 2; ++bi)
+        for (int bi = 0; bi < 2; ++bi) {
+          float gm = acc[bi][bj][0];
 #pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-              const int64_t row = r0 + wr * 64 + bi * 32 + 8 * r4 + 4 * fh;
-              if (row + 3 < n_rows) {
-                f32x4 v = {acc[bi][bj][4 * r4], acc[bi][bj][4 * r4 + 1], acc[bi][bj][4 * r4 + 2],
-                           acc[bi][bj][4 * r4 + 3]};
-                *reinterpret_cast<f32x4*>(score_out + (int64_t)q * score_ld + row) = v;
-              } else {
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                  if (row + u < n_rows) score_out[(int64_t)q * score_ld + row + u] = acc[bi][bj][4 * r4 + u];
-              }
-            }
+          for (int r = 1; r < 16; ++r) gm = fmaxf(gm, acc[bi][bj][r]);
+          const int64_t g = (int64_t)t * 8 + wr * 4 + bi * 2 + fh;
+          if (q < n_q) score_out[(int64_t)q * score_ld + g] = gm;
         }
       }
       __syncthreads();
       continue;
     }
 
+    if (flags & kFlagSkipEpilogue) {  // ablation: GEMM only, keep acc live, no top-k
+      float sink = 0.f;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
+      if (sink == 1234.5678f) part_keys[0] = 1;
+      continue;
+    }
+
     // ---- epilogue: threshold filter -> LDS candidates -> owner merge (repeat on overflow).
-    // Each element test is one compare; the append path is entered only at element positions
-    // where some lane of the wave beats its query's threshold (wave-uniform branch).
-    uint64_t consumed = 0;  // accumulator elements already handed to an owner (bit e)
-    const int row_lane = (int)r0 + wr * 64 + 4 * fh;
+    // Each query's 128 tile scores sit in 4 producer lanes (2 row-waves x 2 lane halves) as 32
+    // registers each. A lane whose 32-score max beats its query's threshold is "flagged" and
+    // spills its 32 scores to a per-wave LDS scratch; the whole wave then screens two flagged
+    // lanes per pass (one score per lane), compacts survivors with a ballot and appends them to
+    // the flagged lane's private kProdCap-slot buffer. No per-element branches, no atomics.
+    uint64_t consumed = 0;  // bit (bj * 32 + v): score v of column bj already handed over
+    const int pid = wr * 2 + fh;
+    float* scr = reinterpret_cast<float*>(smem + kOffScratch) + wave * 64 * 32;
     for (;;) {
       ++round_id;
 #pragma unroll
@@ -279,51 +324,106 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
         for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
           for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[bi][bj][r]);
-        if (__any(m >= ths)) {
+        int c = 0;  // this lane's fill of its producer buffer for column bj, this round
+        uint64_t flagged = __ballot(m >= ths);
+        if (flagged) {
+          if (m >= ths) {
 #pragma unroll
-          for (int bi = 0; bi < 2; ++bi) {
+            for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int e = (bi * 2 + bj) * 16 + r;
-              const bool p = acc[bi][bj][r] >= ths && !((consumed >> e) & 1ull);
-              if (__any(p)) {
-                if (p) {
-                  // The opaque copies keep the key arithmetic inside this rarely taken branch;
-                  // hoisted, it would hold 64 keys live and spill the register file.
-                  float sv = acc[bi][bj][r];
-                  int row = row_lane + (bi * 32 + (r & 3) + 8 * (r >> 2));
-                  asm volatile("" : "+v"(sv), "+v"(row));
-                  const uint64_t key = make_key(sv, row_base + (uint32_t)row);
-                  if (row < n_rows && key > thk) {
-                    const uint32_t pos = atomicAdd(&cnt[ql], 1u);
-                    if (pos < (uint32_t)kCandCap) {
-                      cand[ql * kCandStride + pos] = key;
-                      consumed |= (1ull << e);
-                    }
-                  }
-                }
+              for (int c4 = 0; c4 < 4; ++c4) {
+                f32x4 v4 = {acc[bi][bj][4 * c4], acc[bi][bj][4 * c4 + 1], acc[bi][bj][4 * c4 + 2],
+                            acc[bi][bj][4 * c4 + 3]};
+                *reinterpret_cast<f32x4*>(scr + lane * 32 + bi * 16 + 4 * c4) = v4;
               }
+          }
+          __builtin_amdgcn_wave_barrier();
+          const uint32_t cons_bj = (uint32_t)(consumed >> (bj * 32));
+          const float ths_b = ths;
+          const uint32_t thk_lo = (uint32_t)thk, thk_hi = (uint32_t)(thk >> 32);
+          const int v = lane & 31;
+          const int row_v = (v >> 4) * 32 + (v & 3) + 8 * ((v >> 2) & 3);
+          while (flagged) {
+            const int fA = __builtin_ctzll(flagged);
+            flagged &= flagged - 1;
+            const int fB = flagged ? __builtin_ctzll(flagged) : fA;
+            const bool hasB = flagged != 0;
+            if (hasB) flagged &= flagged - 1;
+            const bool upper = lane >= 32;
+            const bool active = !upper || hasB;
+            const int f = upper ? fB : fA;
+            // the flagged lanes' own state, broadcast through scalar reads
+            const float tsA = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths_b), fA));
+            const float tsB = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths_b), fB));
+            const uint64_t tkA = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fA) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fA);
+            const uint64_t tkB = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fB) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fB);
+            const uint32_t csA = (uint32_t)__builtin_amdgcn_readlane((int)cons_bj, fA);
+            const uint32_t csB = (uint32_t)__builtin_amdgcn_readlane((int)cons_bj, fB);
+            const int cA = __builtin_amdgcn_readlane(c, fA);
+            const int cB = __builtin_amdgcn_readlane(c, fB);
+            const float ts = upper ? tsB : tsA;
+            const uint64_t tk = upper ? tkB : tkA;
+            const uint32_t cs = upper ? csB : csA;
+            const int cf = upper ? cB : cA;
+            const float val = scr[f * 32 + v];
+            const int row = (int)r0 + wr * 64 + 4 * (f >> 5) + row_v;
+            bool pass = active && val >= ts && !((cs >> v) & 1u) && row < n_rows;
+            uint64_t key = 0;
+            if (pass) {
+              key = make_key(val, row_base + (uint32_t)row);
+              pass = key > tk;
+            }
+            const uint64_t bal = __ballot(pass);
+            const uint32_t half = upper ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+            const int rank = __builtin_popcount(half & ((1u << v) - 1u));
+            const int total = __builtin_popcount(half);
+            const bool store = pass && cf + rank < kProdCap;
+            if (store) {
+              const int qf = wq * 64 + bj * 32 + (f & 31);
+              const int pf = wr * 2 + (f >> 5);
+              cand[(qf * 4 + pf) * kProdCap + cf + rank] = key;
+            }
+            const uint64_t sbal = __ballot(store);
+            const int totA = __builtin_popcount((uint32_t)bal);
+            const int totB = __builtin_popcount((uint32_t)(bal >> 32));
+            if (cA + totA > kProdCap || (hasB && cB + totB > kProdCap)) flag[round_id & 1] = round_id;
+            (void)total;
+            if (lane == fA) {
+              c = min(cA + totA, kProdCap);
+              consumed |= (uint64_t)(uint32_t)sbal << (bj * 32);
+            }
+            if (hasB && lane == fB) {
+              c = min(cB + totB, kProdCap);
+              consumed |= (uint64_t)(uint32_t)(sbal >> 32) << (bj * 32);
             }
           }
         }
+        cnt[ql * 4 + pid] = c;
       }
       __syncthreads();
       if (tid < kTileQ) {
-        const uint32_t c = cnt[tid];
-        if (c) {
-          const uint32_t n = c < (uint32_t)kCandCap ? c : (uint32_t)kCandCap;
-          for (uint32_t i = 0; i < n; ++i) list_insert<KCAP>(L, cand[tid * kCandStride + i]);
-          cnt[tid] = 0;
+        bool changed = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int n = cnt[tid * 4 + u];
+          const uint64_t* src = cand + (tid * 4 + u) * kProdCap;
+          for (int i = 0; i < n; ++i) list_insert<KCAP>(L, src[i]);
+          changed |= n > 0;
+        }
+        if (changed) {
           const uint64_t kth = list_at<KCAP>(L, k_out - 1);
           if (kth > thr_key[tid]) {
             thr_key[tid] = kth;
             thr_score[tid] = key_score(kth);
           }
-          if (c > (uint32_t)kCandCap) flag[0] = round_id;
         }
       }
       __syncthreads();
-      if (flag[0] != round_id) break;
+      // Parity slots: a round-R overflow write can never race a slower thread's read of the
+      // round R-1 decision (those read the other slot).
+      if (flag[round_id & 1] != round_id) break;
     }
   }
 
@@ -351,12 +451,7 @@ __global__ __launch_bounds__(64) void merge_kernel(const uint64_t* __restrict__ 
   for (int j = 0; j < KCAP; ++j) L[j] = 0;
   for (int64_t i = lane; i < n; i += 64) list_insert<KCAP>(L, src[i]);
   for (int j = 0; j < k; ++j) {
-    uint64_t best = L[0];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const uint64_t o = shfl_xor_u64(best, off);
-      best = o > best ? o : best;
-    }
+    const uint64_t best = wave_max_u64(L[0]);
     if (best != 0 && L[0] == best) {
 #pragma unroll
       for (int t = 0; t < KCAP - 1; ++t) L[t] = L[t + 1];
@@ -371,34 +466,107 @@ __global__ __launch_bounds__(64) void merge_kernel(const uint64_t* __restrict__ 
   }
 }
 
-// Threshold seed: k-th largest of the S sampled scores of each query (bitonic sort in LDS,
-// one 256-thread workgroup per query, S a power of two <= kSampleMax). The sample rows are
-// corpus rows, so the result is a valid lower bound of the query's final k-th best score.
-constexpr int kSampleMax = 1024;
+// Threshold seed: k-th largest of the G sampled group maxima of each query. Group maxima are
+// scores of distinct corpus rows, so the result is a valid lower bound of the query's final
+// k-th best score.
+constexpr int kSampleMax = 16384;              // sampled rows
+constexpr int kGroupMax = kSampleMax / 16;        // group maxima per query
 
-__global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict__ scores, int S,
-                                                         int k, float* __restrict__ thr) {
-  __shared__ uint32_t v[kSampleMax];
+// One wave per query: the k-th largest ordered value is found bit by bit from the MSB
+// (largest t with #{v >= t} >= k), 32 counting passes over 16 values per lane.
+__global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict__ scores, int S,
+                                                        int k, float* __restrict__ thr) {
   const int q = blockIdx.x;
+  const int lane = threadIdx.x;
   const float* src = scores + (int64_t)q * S;
-  for (int i = threadIdx.x; i < S; i += 256) v[i] = ord_f32(src[i]);
-  __syncthreads();
-  for (int size = 2; size <= S; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < S / 2; i += 256) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool desc = (lo & size) == 0;
-        const uint32_t a = v[lo], b = v[hi];
-        if ((a < b) == desc) {
-          v[lo] = b;
-          v[hi] = a;
-        }
-      }
-      __syncthreads();
+  uint32_t v[kGroupMax / 64];
+#pragma unroll
+  for (int j = 0; j < kGroupMax / 64; ++j) {
+    const int i = lane + 64 * j;
+    v[j] = i < S ? ord_f32(src[i]) : 0u;
+  }
+  uint32_t ans = 0;
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t cand = ans | (1u << b);
+    // count over the wave with ballots: scalar popcounts, no cross-lane data movement
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < kGroupMax / 64; ++j) c += __builtin_popcountll(__ballot(v[j] >= cand));
+    if (c >= k) ans = cand;
+  }
+  if (lane == 0) thr[q] = unord_f32(ans);
+}
+
+// k-way merge when each lane holds one whole list in registers (n_lists <= 64, k_in <= KCAP):
+// no dependent global loads inside the k rounds.
+template <int KCAP>
+__global__ __launch_bounds__(64) void merge_lane_lists_kernel(const uint64_t* __restrict__ in, int n_lists,
+                                                              int k_in, int k, float* __restrict__ scores,
+                                                              int32_t* __restrict__ rows,
+                                                              uint64_t* __restrict__ keys_out) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const uint64_t* src = in + ((int64_t)q * n_lists + lane) * k_in;
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = (lane < n_lists && j < k_in) ? src[j] : 0;
+  for (int j = 0; j < k; ++j) {
+    const uint64_t best = wave_max_u64(L[0]);
+    if (best != 0 && L[0] == best) {
+#pragma unroll
+      for (int t = 0; t < KCAP - 1; ++t) L[t] = L[t + 1];
+      L[KCAP - 1] = 0;
+    }
+    if (lane == 0) {
+      const int64_t o = (int64_t)q * k + j;
+      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
+      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
+      if (keys_out) keys_out[o] = best;
     }
   }
-  if (threadIdx.x == 0) thr[q] = unord_f32(v[k - 1]);
+}
+
+// k-way merge of up to 64*kHeadSlots sorted lists: lane l owns lists l, l+64, ...; each round
+// the lane offers the best of its list heads, the wave max wins and the owning list advances.
+constexpr int kHeadSlots = 8;
+
+__global__ __launch_bounds__(64) void merge_heads_kernel(const uint64_t* __restrict__ in, int n_lists,
+                                                         int k_in, int k, float* __restrict__ scores,
+                                                         int32_t* __restrict__ rows,
+                                                         uint64_t* __restrict__ keys_out) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const uint64_t* base = in + (int64_t)q * n_lists * k_in;
+  uint64_t head[kHeadSlots];
+  int ptr[kHeadSlots];
+#pragma unroll
+  for (int u = 0; u < kHeadSlots; ++u) {
+    const int l = lane + 64 * u;
+    ptr[u] = 0;
+    head[u] = (l < n_lists && k_in > 0) ? base[(int64_t)l * k_in] : 0;
+  }
+  for (int j = 0; j < k; ++j) {
+    uint64_t mine = head[0];
+#pragma unroll
+    for (int u = 1; u < kHeadSlots; ++u) mine = head[u] > mine ? head[u] : mine;
+    const uint64_t best = wave_max_u64(mine);
+    if (best != 0 && mine == best) {
+#pragma unroll
+      for (int u = 0; u < kHeadSlots; ++u) {
+        if (head[u] == best) {
+          const int l = lane + 64 * u;
+          ++ptr[u];
+          head[u] = ptr[u] < k_in ? base[(int64_t)l * k_in + ptr[u]] : 0;
+        }
+      }
+    }
+    if (lane == 0) {
+      const int64_t o = (int64_t)q * k + j;
+      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
+      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
+      if (keys_out) keys_out[o] = best;
+    }
+  }
 }
 
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float v) {
@@ -411,7 +579,7 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float v) {
 __device__ __forceinline__ int f32_perm(int j) { return (j & ~7) | ((j & 1) << 2) | ((j >> 1) & 3); }
 
 // fp32 rows -> storage rows (one wave per row): optional L2 normalisation, dtype conversion,
-// zero padding to d_pad, fp32 lane permutation.
+// zero padding to d_pad, fp32 lane permutation. Lanes move 4 consecutive elements at a time.
 __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restrict__ src, int64_t n,
                                                            int dim, const int64_t* __restrict__ slots,
                                                            int64_t start, int normalize,
@@ -422,25 +590,48 @@ __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restri
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   if (i >= n) return;
   const float* x = src + i * dim;
+  const bool vec = (dim & 3) == 0;
   float nrm = 1.f;
   if (normalize) {
     float s = 0.f;
-    for (int j = lane; j < dim; j += 64) s = fmaf(x[j], x[j], s);
+    if (vec) {
+      for (int j = 4 * lane; j < dim; j += 256) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(x + j);
+        s = fmaf(v[0], v[0], s); s = fmaf(v[1], v[1], s); s = fmaf(v[2], v[2], s); s = fmaf(v[3], v[3], s);
+      }
+    } else {
+      for (int j = lane; j < dim; j += 64) s = fmaf(x[j], x[j], s);
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
     nrm = fmaxf(sqrtf(s), 1e-12f);
   }
   const int64_t slot = slots ? slots[i] : start + i;
   uint8_t* row = dst + slot * row_stride;
-  for (int j = lane; j < d_pad; j += 64) {
-    float v = j < dim ? x[j] : 0.f;
-    if (normalize) v = v / nrm;
-    if (dt == DT_BF16) {
-      reinterpret_cast<uint16_t*>(row)[j] = f32_to_bf16_rne(v);
-    } else if (dt == DT_F16) {
-      reinterpret_cast<_Float16*>(row)[j] = (_Float16)v;
+  for (int j = 4 * lane; j < d_pad; j += 256) {
+    f32x4 v;
+    if (vec && j + 3 < dim) {
+      v = *reinterpret_cast<const f32x4*>(x + j);
     } else {
-      reinterpret_cast<float*>(row)[f32_perm(j)] = v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (j + u < dim) ? x[j + u] : 0.f;
+    }
+    if (normalize) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = v[u] / nrm;
+    }
+    if (dt == DT_BF16) {
+      uint2 w;
+      w.x = (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16);
+      w.y = (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16);
+      *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
+    } else if (dt == DT_F16) {
+      _Float16* o = reinterpret_cast<_Float16*>(row) + j;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = (_Float16)v[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) reinterpret_cast<float*>(row)[f32_perm(j + u)] = v[u];
     }
   }
 }
@@ -491,7 +682,8 @@ struct ahr_index {
   int64_t part_cap = 0;  // uint64 elements
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
   int64_t sample_cap = 0;   // floats
-  int sample_rows = 1024;   // S; 0 disables the threshold pre-pass
+  int sample_rows = 8192;   // S; 0 disables the threshold pre-pass
+  int debug_flags = 0;      // ablation flags (kFlagSkipEpilogue); 0 in production
   // Optional stage timing: a ring of HIP events, kStages+1 per query call, recorded on the
   // call's stream (ahr_index_profile_begin / _end).
   std::vector<hipEvent_t> prof_events;
@@ -526,16 +718,24 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 
 struct SearchPlan {
   int qblocks, n_row_tiles, n_splits, tiles_per_split;
+  bool xcd_remap;
 };
+
+// Resident workgroups of the tile kernel per CU (VGPR-limited to 2 waves/SIMD, 4-wave groups).
+constexpr int kResidentSlots = 256 * 2;
 
 SearchPlan plan_search(const ahr_index* ix, int B) {
   SearchPlan p;
   p.qblocks = (int)cdiv(B, kTileQ);
   p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
-  const int target_wgs = 1024;
-  int splits = (int)std::max<int64_t>(1, std::min<int64_t>(p.n_row_tiles, cdiv(target_wgs, p.qblocks)));
-  p.tiles_per_split = std::max(1, (int)cdiv(p.n_row_tiles, splits));
+  // One wave of workgroups that fills every resident slot; splits padded to a multiple of 8
+  // so the XCD remap keeps a split's query blocks on one XCD.
+  int64_t want = std::max<int64_t>(1, cdiv(kResidentSlots, p.qblocks));
+  want = std::min<int64_t>(want, std::max(1, p.n_row_tiles));
+  p.tiles_per_split = std::max(1, (int)cdiv(p.n_row_tiles, want));
   p.n_splits = std::max(1, (int)cdiv(p.n_row_tiles, p.tiles_per_split));
+  p.xcd_remap = p.n_splits >= 8;
+  if (p.xcd_remap) p.n_splits = (int)cdiv(p.n_splits, 8) * 8;
   return p;
 }
 
@@ -551,10 +751,9 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
     ix->q_cap = q_need;
   }
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
-  const int64_t max_tiles = std::max<int64_t>(1, ix->cap_pad / kTileRows);
   const int64_t qblocks = cdiv(B, kTileQ);
-  const int64_t max_splits = std::min<int64_t>(max_tiles, cdiv(1024, qblocks));
-  const int64_t p_need = (int64_t)B * max_splits * k;
+  const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlots, qblocks)), 8) * 8;
+  const int64_t p_need = (int64_t)B * std::max<int64_t>(max_splits, kSampleMax / kTileRows) * k;
   if (p_need > ix->part_cap) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
     ix->part = nullptr;
@@ -563,7 +762,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
       return fail(AHR_ENOMEM, "partial top-k workspace allocation failed");
     ix->part_cap = p_need;
   }
-  const int64_t s_need = (int64_t)B * (kSampleMax + 1);
+  const int64_t s_need = (int64_t)B * (kGroupMax + 1);
   if (s_need > ix->sample_cap) {
     if (ix->sample) AHR_HIP(hipFree(ix->sample));
     ix->sample = nullptr;
@@ -578,17 +777,18 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
 template <int DT, int KCAP, int MODE>
 void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_split,
                  int n_row_tiles, int n_rows, int B, int k, uint32_t row_base, const float* thr,
-                 float* score_out, int64_t score_ld, hipStream_t s) {
+                 float* score_out, int64_t score_ld, int flags, hipStream_t s) {
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs the opt-in once per kernel
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tile_kernel<DT, KCAP, MODE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr_set = true;
   }
-  dim3 grid(n_splits, qblocks);
+  dim3 grid((unsigned)(n_splits * qblocks));
   hipLaunchKernelGGL((topk_tile_kernel<DT, KCAP, MODE>), grid, dim3(kThreads), kLdsBytes, s,
                      ix->rows, ix->qbuf, ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes,
-                     tiles_per_split, n_row_tiles, row_base, k, ix->part, thr, score_out, score_ld);
+                     tiles_per_split, n_row_tiles, row_base, k, ix->part, thr, score_out, score_ld,
+                     n_splits, qblocks, flags);
 }
 
 template <int DT>
@@ -597,26 +797,42 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const float* thr = nullptr;
   prof_mark(ix, 1, s);
   const int S = ix->sample_rows;
-  if (S > 0 && ix->count >= 8 * (int64_t)S) {
+  if (S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
     // Threshold pre-pass: score the first S rows, take each query's k-th best.
     float* scores = ix->sample;
-    float* t = ix->sample + (int64_t)B * S;
-    launch_tile<DT, 8, MODE_STORE>(ix, S / kTileRows, p.qblocks, 1, S / kTileRows, S, B, k, 0,
-                                   nullptr, scores, S, s);
-    hipLaunchKernelGGL(sample_kth_kernel, dim3(B), dim3(256), 0, s, scores, S, k, t);
+    float* t = ix->sample + (int64_t)B * (S / 16);
+    const int G = S / 16;  // 16-row groups
+    launch_tile<DT, 8, MODE_GROUPMAX>(ix, S / kTileRows, p.qblocks, 1, S / kTileRows, S, B, k, 0,
+                                      nullptr, scores, G, 0, s);
+    hipLaunchKernelGGL(sample_kth_kernel, dim3(B), dim3(64), 0, s, scores, G, k, t);
     thr = t;
   }
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
+  const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
   switch (kcap_for(k)) {
-    case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
-    case 16: launch_tile<DT, 16, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
-    default: launch_tile<DT, 32, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, s); break;
+    case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
+    case 16: launch_tile<DT, 16, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
+    default: launch_tile<DT, 32, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
   }
 }
 
 void launch_merge(const uint64_t* in, int B, int n_lists, int k_in, int k, float* scores,
                   int32_t* rows, uint64_t* keys_out, hipStream_t s) {
+  if (n_lists <= 64 && k_in <= 32) {
+    const int kc = kcap_for(k_in);
+    if (kc == 8)
+      hipLaunchKernelGGL((merge_lane_lists_kernel<8>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+    else if (kc == 16)
+      hipLaunchKernelGGL((merge_lane_lists_kernel<16>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+    else
+      hipLaunchKernelGGL((merge_lane_lists_kernel<32>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+    return;
+  }
+  if (n_lists <= 64 * kHeadSlots) {
+    hipLaunchKernelGGL(merge_heads_kernel, dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+    return;
+  }
   switch (kcap_for(k)) {
     case 8:
       hipLaunchKernelGGL((merge_kernel<8>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
@@ -830,9 +1046,15 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum, int* n_calls) {
 
 int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  if (rows < 0 || rows > kSampleMax || (rows & (rows - 1)) || (rows && rows < kTileRows))
-    return fail(AHR_EINVAL, "sample rows must be 0 or a power of two in [128, 1024]");
+  if (rows < 0 || rows > kSampleMax || (rows & (rows - 1)) || (rows && rows < 256))
+    return fail(AHR_EINVAL, "sample rows must be 0 or a power of two in [256, 16384]");
   ix->sample_rows = rows;
+  return AHR_OK;
+}
+
+int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  ix->debug_flags = flags & kFlagSkipEpilogue;
   return AHR_OK;
 }
 

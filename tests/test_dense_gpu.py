@@ -38,7 +38,8 @@ def _run(index_dtype, C, Q, k, cuda):
 
 @pytest.mark.parametrize("n,d,B,k", [
     (1, 768, 1, 1), (100, 768, 3, 5), (1000, 384, 7, 10), (5000, 768, 130, 10),
-    (20000, 768, 64, 16), (9000, 100, 5, 32), (300, 768, 129, 8)])
+    (20000, 768, 64, 16), (9000, 100, 5, 32), (300, 768, 129, 8),
+    (40000, 768, 200, 10), (33000, 384, 1, 32)])  # >= 8*4096 rows: threshold pre-pass path
 def test_f32_bit_exact(cuda, n, d, B, k):
     rng = np.random.default_rng(1000 + n + d + B + k)
     C = _clustered(rng, n, d)
@@ -53,7 +54,8 @@ def test_f32_bit_exact(cuda, n, d, B, k):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("n,d,B,k", [(4000, 768, 17, 10), (20000, 768, 256, 10), (12000, 384, 33, 5)])
+@pytest.mark.parametrize("n,d,B,k", [(4000, 768, 17, 10), (20000, 768, 256, 10), (12000, 384, 33, 5),
+                                     (50000, 768, 300, 10)])
 def test_half_precision_vs_f64(cuda, dtype, n, d, B, k):
     rng = np.random.default_rng(7 + n + B)
     C = dr.round_to_storage(_clustered(rng, n, d), dtype)
@@ -152,3 +154,33 @@ def test_merge_matches_single_shard(cuda):
         s, r, _ = merge_topk_keys(keys, 10)
         np.testing.assert_array_equal(r.cpu().numpy(), full_r)
         np.testing.assert_array_equal(s.cpu().numpy(), full_s)
+
+
+def test_prepass_disabled_same_result(cuda):
+    """The threshold pre-pass only prunes work: results equal with it switched off."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(9)
+    C = _clustered(rng, 40000, 768)
+    Q = _clustered(rng, 100, 768)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    a = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    ix.set_sample_rows(0)
+    b = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    ix.set_sample_rows(256)
+    c = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    ix.close()
+    for x, y in ((a, b), (a, c)):
+        np.testing.assert_array_equal(x[0], y[0])
+        np.testing.assert_array_equal(x[1], y[1])
+
+
+def test_many_lists_merge(cuda):
+    """Small batches use hundreds of row splits: the heads merge must still be exact."""
+    rng = np.random.default_rng(10)
+    C = _clustered(rng, 60000, 384)
+    Q = _clustered(rng, 3, 384)
+    s, r = _run("f32", C, Q, 32, cuda)
+    es, er = dr.topk(C, Q, 32, mode="fma")
+    np.testing.assert_array_equal(r, er)
+    np.testing.assert_array_equal(s, es.astype(np.float32))

@@ -1,0 +1,73 @@
+"""Ablation timings of the dense search stages on one GPU (interleaved variants, one process).
+
+Variants: production; no threshold pre-pass; GEMM only (epilogue skipped, wrong output).
+Prints per-stage milliseconds (HIP events on the query stream) per variant and batch size.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ah-rag_amd"), ROOT]
+
+import torch  # noqa: E402
+
+from ah_rag.embeddings import DenseIndex  # noqa: E402
+from ah_rag.synthetic import HOTPOT_90K, SYNTH_5M, SyntheticCorpus  # noqa: E402
+
+
+def run(ix, q, k, steps):
+    for _ in range(3):
+        ix.query(q, k)
+    torch.cuda.synchronize()
+    ix.profile_begin(steps)
+    for _ in range(steps):
+        ix.query(q, k)
+    torch.cuda.synchronize()
+    p = ix.profile_end()
+    return {s: round(v / p["calls"], 4) for s, v in p["ms_sum"].items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="hotpot90k")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--batches", default="1,64,256,1024,4096")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    spec = HOTPOT_90K if a.workload == "hotpot90k" else SYNTH_5M
+    c = SyntheticCorpus(spec, dev)
+    rows = c.rows()
+    ix = DenseIndex(rows.shape[1], rows.shape[0], dtype=a.dtype, device=dev)
+    for s in range(0, rows.shape[0], 1_000_000):
+        ix.upsert(rows[s:s + 1_000_000], start=s)
+    out = []
+    for B in [int(x) for x in a.batches.split(",")]:
+        q, _ = c.queries(B, rows)
+        res = {}
+        for r in range(a.rounds):
+            for name, sample, flags in (("prod", 8192, 0), ("s4096", 4096, 0), ("s16384", 16384, 0),
+                                        ("no_prepass", 0, 0), ("gemm_only", 0, 2)):
+                ix.set_sample_rows(sample)
+                ix.set_debug_flags(flags)
+                t = run(ix, q, a.k, a.steps)
+                res.setdefault(name, []).append(t)
+        ix.set_sample_rows(8192)
+        ix.set_debug_flags(0)
+        best = {n: min(v, key=lambda d: sum(d.values())) for n, v in res.items()}
+        flops = 2.0 * B * rows.shape[0] * rows.shape[1]
+        line = {"B": B, "plan": ix.plan(B)}
+        for n, t in best.items():
+            line[n] = t
+            line[n + "_tile_TFs"] = round(flops / (t["tile_topk"] * 1e-3) / 1e12, 1)
+            line[n + "_qps"] = round(B / (sum(t.values()) * 1e-3))
+        out.append(line)
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
