@@ -1,0 +1,347 @@
+"""GraphEnvironment — drop-in for reference src/ah_rag/agent/environment.py (class at :15).
+
+Same constructor, actions, observation and info dicts. The differences are where the time goes:
+  * neighbour expansions (expand_parents / expand_children / expand_related, reference :393-480)
+    run as the batched HIP kernel ahr_graph_expand over the device CSR (B = 1 here;
+    VecGraphEnvironment in ah_rag.agent.vec_env batches them across environments);
+  * semantic_anchor goes through HierarchicalGraph.search (dense top-k + expansion + rerank on the
+    GPU);
+  * the node/edge counts every observation reports (reference :136-139, an O(N) networkx walk per
+    step) are computed once per graph version;
+  * expand_to_lca (reference :243-299, which rebuilds the belongs_to subgraph on every call) walks
+    the cached belongs_to CSR mirror on the host: ancestor sets here are a handful of nodes.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+import uuid
+from collections import deque
+from datetime import datetime
+from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
+
+import networkx as nx
+import numpy as np
+import torch
+
+from ..graph.hierarchical_graph import HierarchicalGraph
+from ..graph_search import parse_judge
+
+ADJ_BT_OUT, ADJ_BT_IN = 0, 1
+
+
+class GraphEnvironment:
+    """Action API over a HierarchicalGraph: reset, semantic_anchor, expansions, LCA, details,
+    selection/frontier state, dynamic filters and weights, session logging."""
+
+    def __init__(self, graph_dir: str = "graph", random_state: int = 42,
+                 logging_enabled: bool = True, log_dir: str = "artifacts/phase2", session_id: Optional[str] = None,
+                 debug: bool = False, log_level: str = "normal", redact: bool = True) -> None:
+        self.graph_dir = graph_dir
+        self.random_state = random_state
+        self.hg: Optional[HierarchicalGraph] = None
+        self.last_query: Optional[str] = None
+        self.last_results: Optional[Dict[str, Any]] = None
+        self.step_count = 0
+        self.selection_set: Set[str] = set()
+        self.frontier_set: Set[str] = set()
+        self.current_filters: Dict[str, Any] = {"judge_overall_min": None, "confidence_min": None,
+                                                "type_filter": None}
+        self.current_weights: Dict[str, Any] = {"alpha": None, "beta": None, "gamma": None, "delta": None,
+                                                "member_top_m": None, "top_k": 5}
+        self.logging_enabled = logging_enabled
+        self.log_dir = log_dir
+        self.session_id = session_id or datetime.utcnow().strftime("%Y%m%dT%H%M%S") + "-" + uuid.uuid4().hex[:6]
+        self.session_path = os.path.join(log_dir, self.session_id)
+        self.debug = debug
+        self.stats: Dict[str, Any] = {"actions": [], "cumulative": {"steps": 0, "queries": 0, "expansions": 0,
+                                                                   "time_s": 0.0}}
+        self.logger = None
+        if logging_enabled:
+            from ..utils.logging_init import get_logger
+            self.logger = get_logger(self.session_path, self.session_id, level=log_level, redact=redact)
+            try:
+                with open(os.path.join(self.session_path, "session.json"), "w", encoding="utf-8") as f:
+                    json.dump({"session_id": self.session_id, "created_at": datetime.utcnow().isoformat() + "Z"}, f)
+            except Exception:
+                pass
+        self._count_cache: Optional[Tuple[Tuple, Dict[str, int]]] = None
+        self._dag_cache: Optional[Tuple[Tuple, bool, Set[str]]] = None
+        self._ensure_graph_loaded()
+
+    # ---- plumbing ----------------------------------------------------------------------------
+    def _ensure_graph_loaded(self) -> None:
+        if self.hg is None:
+            self.hg = HierarchicalGraph.load(self.graph_dir)
+
+    def _log(self, event: Dict[str, Any]) -> None:
+        if self.logging_enabled and self.logger is not None:
+            try:
+                self.logger.info(**{**event, "step": self.step_count})
+            except Exception:
+                pass
+
+    def _record(self, info: Dict[str, Any], expansion: bool = False, query_time: Optional[float] = None) -> None:
+        self.stats["actions"].append(info)
+        cum = self.stats["cumulative"]
+        cum["steps"] += 1
+        if expansion:
+            cum["expansions"] += 1
+        if query_time is not None:
+            cum["queries"] += 1
+            cum["time_s"] += query_time
+
+    def _counts(self) -> Dict[str, int]:
+        stamp = self.hg._graph_stamp()
+        if self._count_cache is None or self._count_cache[0] != stamp:
+            self._count_cache = (stamp, {"n_nodes": self.hg.G.number_of_nodes(),
+                                         "n_edges": self.hg.G.number_of_edges()})
+        return dict(self._count_cache[1])
+
+    def _node_brief(self, node_id: str) -> Dict[str, Any]:
+        d = self.hg.G.nodes.get(node_id, {})
+        kind = d.get("node_type")
+        return {"node_id": node_id, "node_type": kind, "entity_type": d.get("entity_type"),
+                "layer": 0 if kind == "entity" else (d.get("level") or (1 if kind == "summary" else 0)),
+                "title": d.get("title"), "name": d.get("name"),
+                "judge_overall": parse_judge(d.get("judge_scores")), "confidence": d.get("confidence")}
+
+    def _brief_scored(self, res: Dict[str, Any]) -> Dict[str, Any]:
+        b = self._node_brief(res.get("node_id"))
+        b["score"] = res.get("score")
+        b["semantic"] = res.get("semantic")
+        return b
+
+    def _observation(self, seeds: List[Dict[str, Any]], reranked: List[Dict[str, Any]]) -> Dict[str, Any]:
+        obs: Dict[str, Any] = {
+            "selection": [self._brief_scored(x) for x in reranked],
+            "seeds": [self._brief_scored(x) for x in seeds],
+            "state": {"selection_ids": sorted(self.selection_set),
+                      "frontier_ids": sorted(self.frontier_set)[:50]},
+            "counts": self._counts(),
+            "step": self.step_count,
+        }
+        if self.debug:
+            obs["diagnostics"] = {"filters": self.current_filters, "weights": self.current_weights,
+                                  "last_query": self.last_query, "frontier_size": len(self.frontier_set),
+                                  "selection_size": len(self.selection_set)}
+        return obs
+
+    def _bare_observation(self, selection: List[Dict[str, Any]]) -> Dict[str, Any]:
+        return {"selection": selection, "seeds": [], "counts": self._counts(), "step": self.step_count}
+
+    # ---- core API ----------------------------------------------------------------------------
+    def reset(self, seed_query: Optional[str] = None, top_k: int = 5) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        self._ensure_graph_loaded()
+        self.last_query = None
+        self.last_results = None
+        self.step_count = 0
+        self.selection_set.clear()
+        self.frontier_set.clear()
+        if seed_query:
+            return self.semantic_anchor(seed_query, top_k=top_k)
+        self._log({"action": "reset", "message": "reset without seed_query"})
+        return self._bare_observation([]), {"message": "reset without seed_query"}
+
+    def _search_kwargs(self, top_k, member_top_m, judge_overall_min, confidence_min, type_filter):
+        f, w = self.current_filters, self.current_weights
+        return {"top_k": top_k, "member_top_m": member_top_m,
+                "judge_overall_min": f.get("judge_overall_min") if judge_overall_min is None else judge_overall_min,
+                "confidence_min": f.get("confidence_min") if confidence_min is None else confidence_min,
+                "type_filter": f.get("type_filter") if type_filter is None else type_filter,
+                "alpha": w.get("alpha"), "beta": w.get("beta"), "gamma": w.get("gamma"), "delta": w.get("delta")}
+
+    def semantic_anchor(self, query: str, top_k: int = 5, member_top_m: int = 5,
+                        judge_overall_min: Optional[float] = None, confidence_min: Optional[float] = None,
+                        type_filter: Optional[List[str]] = None) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        self._ensure_graph_loaded()
+        self.step_count += 1
+        self.last_query = query
+        kw = self._search_kwargs(top_k, member_top_m, judge_overall_min, confidence_min, type_filter)
+        t0 = time.perf_counter()
+        cluster = self.hg.search(query=query, return_cluster=True, **kw)
+        dur = time.perf_counter() - t0
+        return self._anchor_result(query, top_k, cluster, dur)
+
+    def _anchor_result(self, query: str, top_k: int, cluster: Dict[str, Any], dur: float):
+        seeds = cluster.get("seeds", [])
+        reranked = cluster.get("reranked", [])
+        self.frontier_set = {x.get("node_id") for x in reranked if x.get("node_id")}
+        obs = self._observation(seeds, reranked)
+        info = {"action": "semantic_anchor", "query": query, "top_k": top_k, "returned": len(reranked),
+                "time_s": round(dur, 4)}
+        self.last_results = cluster
+        self._log({**info, "filters": self.current_filters, "weights": self.current_weights})
+        self._record(info, query_time=dur)
+        return obs, info
+
+    # ---- LCA over belongs_to (reference :243-299) ---------------------------------------------
+    def _belongs_to_dag(self) -> Tuple[bool, Set[str]]:
+        """(is_acyclic, nodes touching a belongs_to edge) — cached per graph version."""
+        stamp = self.hg._graph_stamp()
+        if self._dag_cache is None or self._dag_cache[0] != stamp:
+            dg = self.hg.device_graph()
+            n = dg.n_nodes
+            out_off, out_tgt = dg._offsets[ADJ_BT_OUT], dg._targets[ADJ_BT_OUT]
+            indeg = np.zeros(n, np.int64)
+            members: Set[int] = set()
+            for u in range(n):
+                for v in out_tgt[out_off[u]:out_off[u + 1]]:
+                    indeg[v] += 1
+                    members.add(u)
+                    members.add(int(v))
+            # Kahn's algorithm restricted to nodes that carry a belongs_to edge
+            queue = deque(u for u in members if indeg[u] == 0)
+            seen = 0
+            while queue:
+                u = queue.popleft()
+                seen += 1
+                for v in out_tgt[out_off[u]:out_off[u + 1]]:
+                    indeg[v] -= 1
+                    if indeg[v] == 0:
+                        queue.append(int(v))
+            self._dag_cache = (stamp, seen == len(members), {dg.ids[i] for i in members})
+        return self._dag_cache[1], self._dag_cache[2]
+
+    def _ancestors_or_self(self, node_id: str) -> Set[str]:
+        """Nodes with a belongs_to path TO node_id, plus itself (nx.ancestors on the belongs_to DAG)."""
+        dg = self.hg.device_graph()
+        start = dg.index[node_id]
+        seen = {start}
+        stack = [start]
+        while stack:
+            u = stack.pop()
+            for v in dg.neighbors(u, ADJ_BT_IN):
+                v = int(v)
+                if v not in seen:
+                    seen.add(v)
+                    stack.append(v)
+        return {dg.ids[i] for i in seen}
+
+    def expand_to_lca(self, node_ids: List[str], max_results: int = 5) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        self._ensure_graph_loaded()
+        self.step_count += 1
+        is_dag, dag_nodes = self._belongs_to_dag()
+        sets = []
+        for nid in node_ids:
+            if nid not in dag_nodes:
+                raise nx.NetworkXError(f"The node {nid} is not in the digraph.")
+            sets.append(self._ancestors_or_self(nid))
+        inter = set.intersection(*sets) if sets else set()
+        G = self.hg.G
+        lowest = [n for n in inter
+                  if not any(a.get("edge_type") == "belongs_to" and v in inter for v, a in G.succ[n].items())]
+        t0 = time.perf_counter()
+        picked = sorted(lowest, key=lambda x: (G.nodes[x].get("level") or 1, x))[:max_results]
+        obs = self._observation([{"node_id": n, "semantic": 0.0} for n in picked],
+                                [{"node_id": n, "score": 0.0, "semantic": 0.0} for n in picked])
+        info = {"action": "expand_to_lca", "inputs": node_ids, "lca_count": len(picked), "dag": is_dag,
+                "time_s": round(time.perf_counter() - t0, 4)}
+        self._log(info)
+        self._record(info, expansion=True)
+        return obs, info
+
+    def query_node_details(self, node_id: str) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        self._ensure_graph_loaded()
+        self.step_count += 1
+        if node_id not in self.hg.G:
+            return self._bare_observation([]), {"error": "node_not_found", "node_id": node_id}
+        d = self.hg.G.nodes[node_id]
+        details = {**self._node_brief(node_id), "title": d.get("title"), "name": d.get("name"),
+                   "summary_text": (d.get("summary_text") or d.get("summary") or "")[:500],
+                   "description": (d.get("description") or "")[:500],
+                   "top_words": d.get("top_words"), "members": d.get("members")}
+        info = {"action": "query_node_details", "node_id": node_id}
+        self._log(info)
+        self._record(info)
+        return self._bare_observation([details]), info
+
+    # ---- state & dynamic params --------------------------------------------------------------
+    def commit_selection(self, node_ids: List[str]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        self._ensure_graph_loaded()
+        self.step_count += 1
+        added = []
+        for nid in node_ids:
+            if nid in self.hg.G and nid not in self.selection_set:
+                self.selection_set.add(nid)
+                added.append(nid)
+                self.frontier_set.discard(nid)
+        obs = self._observation([], [{"node_id": n, "score": 0.0, "semantic": 0.0} for n in added])
+        info = {"action": "commit_selection", "added": added, "total_selection": len(self.selection_set)}
+        self._log(info)
+        self._record(info)
+        return obs, info
+
+    def set_filters(self, judge_overall_min: Optional[float] = None, confidence_min: Optional[float] = None,
+                    type_filter: Optional[List[str]] = None) -> Dict[str, Any]:
+        if judge_overall_min is not None:
+            self.current_filters["judge_overall_min"] = judge_overall_min
+        if confidence_min is not None:
+            self.current_filters["confidence_min"] = confidence_min
+        if type_filter is not None:
+            self.current_filters["type_filter"] = list(type_filter)
+        info = {"action": "set_filters", **self.current_filters}
+        self._log(info)
+        self.stats["actions"].append(info)
+        return info
+
+    def set_search_weights(self, alpha: Optional[float] = None, beta: Optional[float] = None,
+                           gamma: Optional[float] = None, delta: Optional[float] = None,
+                           member_top_m: Optional[int] = None, top_k: Optional[int] = None) -> Dict[str, Any]:
+        for key, val in (("alpha", alpha), ("beta", beta), ("gamma", gamma), ("delta", delta),
+                         ("member_top_m", member_top_m), ("top_k", top_k)):
+            if val is not None:
+                self.current_weights[key] = val
+        info = {"action": "set_search_weights", **self.current_weights}
+        self._log(info)
+        self.stats["actions"].append(info)
+        return info
+
+    # ---- expansions (device kernel) ----------------------------------------------------------
+    def _expand(self, action: str, node_ids: List[str], limit: int) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        self._ensure_graph_loaded()
+        self.step_count += 1
+        dg = self.hg.device_graph()
+        idx = torch.from_numpy(dg.node_indices(node_ids).reshape(1, -1)) if node_ids else \
+            torch.full((1, 1), -1, dtype=torch.int32)
+        out, cnt = dg.expand(action, idx, limit)
+        n = int(cnt[0].item())
+        ids = [dg.ids[i] for i in out[0, :n].tolist()]
+        obs = self._observation([{"node_id": x, "semantic": 0.0} for x in ids],
+                                [{"node_id": x, "score": 0.0, "semantic": 0.0} for x in ids])
+        info = {"action": "expand_" + action, "inputs": node_ids, "returned": len(ids)}
+        self.frontier_set.update(ids)
+        self._log(info)
+        self._record(info, expansion=True)
+        return obs, info
+
+    def expand_children(self, node_ids: List[str], limit: int = 10) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        return self._expand("children", node_ids, limit)
+
+    def expand_parents(self, node_ids: List[str], limit: int = 10) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        return self._expand("parents", node_ids, limit)
+
+    def expand_related(self, node_ids: List[str], limit: int = 10) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        return self._expand("related", node_ids, limit)
+
+    # ---- debug & episode end -----------------------------------------------------------------
+    def set_debug(self, enabled: bool = True) -> Dict[str, Any]:
+        self.debug = enabled
+        info = {"action": "set_debug", "debug": self.debug}
+        self._log(info)
+        self.stats["actions"].append(info)
+        return info
+
+    def end_episode(self) -> Dict[str, Any]:
+        summary = {"session_id": self.session_id, "created_at": datetime.utcnow().isoformat() + "Z",
+                   "selection_size": len(self.selection_set), "frontier_size": len(self.frontier_set),
+                   "stats": self.stats, "filters": self.current_filters, "weights": self.current_weights,
+                   "last_query": self.last_query}
+        try:
+            with open(os.path.join(self.session_path, "summary.json"), "w", encoding="utf-8") as f:
+                json.dump(summary, f, ensure_ascii=False, indent=2)
+        except Exception:
+            pass
+        self._log({"action": "end_episode"})
+        return summary

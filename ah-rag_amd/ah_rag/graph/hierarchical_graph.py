@@ -1,0 +1,531 @@
+"""HierarchicalGraph — drop-in for reference src/ah_rag/graph/hierarchical_graph.py (class at :21).
+
+The graph model (networkx DiGraph of entity / hyperedge / summary nodes, node-link JSON
+persistence) keeps the reference's data format, so graphs saved by either implementation load
+in the other. What changes is the retrieval core behind the same signatures:
+
+  build_vector_index  (reference :602-673) encodes node texts once and writes an on-disk vector
+                      store (`<db_path>/ahr_vectors.npy` + `ahr_rows.json`) instead of a Chroma
+                      SQLite collection, with the same sha1 upsert-only bookkeeping in
+                      G.graph["vector_index"]["indexed_meta"];
+  search              (reference :675-789) runs dense top-k, 1-hop expansion and rerank on the
+                      MI355X (ah_rag.graph_search.SearchEngine -> libahr_hip.so) and only builds
+                      the result dicts on the host. search_batch() answers many queries per call.
+
+Not carried over: build_from_artifacts (:241-421, LLM/BERTopic ingest; SURVEY §2 marks it out of
+scope) raises NotImplementedError.
+
+Caching: the device index and device graph are built on first search and reused. Mutations made
+through this class's add_* methods invalidate them; after editing self.G directly, call
+invalidate_device_cache().
+"""
+from __future__ import annotations
+
+import copy
+import datetime
+import hashlib
+import json
+import os
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import networkx as nx
+import numpy as np
+import torch
+
+from ..embeddings import DEFAULT_MODEL, DenseIndex, load_encoder
+from ..graph_search import (DeviceGraph, SEARCH_DEFAULTS, SearchEngine, parse_judge,
+                            resolve_search_params)
+from .. import _native as nat
+
+ARTIFACT_DIR = "artifacts"
+GRAPH_DIR = "graph"
+STRUCTURE_FILE = os.path.join(GRAPH_DIR, "structure.json")
+META_FILE = os.path.join(GRAPH_DIR, "meta.json")
+
+VECTORS_FILE = "ahr_vectors.npy"
+ROWS_FILE = "ahr_rows.json"
+
+
+def _sha(text: str) -> str:
+    return hashlib.sha1(text.encode("utf-8")).hexdigest()
+
+
+class VectorStore:
+    """The persisted node-vector collection (Chroma's role): rows of (id, fp32 vector, metadata)."""
+
+    def __init__(self, path: str) -> None:
+        self.path = path
+        self.ids: List[str] = []
+        self.metas: List[Dict[str, Any]] = []
+        self.vectors = np.zeros((0, 0), np.float32)
+        self.model: Optional[str] = None
+        vp, rp = os.path.join(path, VECTORS_FILE), os.path.join(path, ROWS_FILE)
+        if os.path.exists(vp) and os.path.exists(rp):
+            with open(rp, encoding="utf-8") as f:
+                rows = json.load(f)
+            self.ids, self.metas, self.model = rows["ids"], rows["metadatas"], rows.get("model")
+            self.vectors = np.load(vp, allow_pickle=False)
+
+    def clear(self) -> None:
+        self.ids, self.metas = [], []
+        self.vectors = np.zeros((0, 0), np.float32)
+
+    def upsert(self, ids: Sequence[str], vectors: np.ndarray, metas: Sequence[Dict[str, Any]]) -> None:
+        slot = {nid: i for i, nid in enumerate(self.ids)}
+        if self.vectors.size == 0:
+            self.vectors = np.zeros((0, vectors.shape[1]), np.float32)
+        if vectors.shape[1] != self.vectors.shape[1]:
+            raise ValueError("embedding dimension differs from the stored collection")
+        new_rows = []
+        for nid, v, m in zip(ids, vectors, metas):
+            if nid in slot:
+                self.vectors[slot[nid]] = v
+                self.metas[slot[nid]] = dict(m)
+            else:
+                slot[nid] = len(self.ids) + len(new_rows)
+                new_rows.append((nid, v, m))
+        if new_rows:
+            self.ids += [r[0] for r in new_rows]
+            self.metas += [dict(r[2]) for r in new_rows]
+            self.vectors = np.concatenate([self.vectors, np.stack([r[1] for r in new_rows])]).astype(np.float32)
+
+    def save(self, model: str) -> None:
+        os.makedirs(self.path, exist_ok=True)
+        self.model = model
+        np.save(os.path.join(self.path, VECTORS_FILE), self.vectors.astype(np.float32), allow_pickle=False)
+        with open(os.path.join(self.path, ROWS_FILE), "w", encoding="utf-8") as f:
+            json.dump({"model": model, "ids": self.ids, "metadatas": self.metas}, f, ensure_ascii=False)
+
+    def stamp(self) -> Tuple:
+        try:
+            st = os.stat(os.path.join(self.path, VECTORS_FILE))
+            return (st.st_mtime_ns, st.st_size)
+        except OSError:
+            return (0, 0)
+
+
+class HierarchicalGraph:
+    """Unified DiGraph of L0 entities, L0 hyperedges and L1+ summaries (attributes on nodes/edges)."""
+
+    def __init__(self) -> None:
+        self.G: nx.DiGraph = nx.DiGraph()
+        self.name_to_entity_id: Dict[str, str] = {}
+        self.topic_to_summary_id: Dict[int, str] = {}
+        self._query_embedder_name: Optional[str] = None
+        self._query_embedder = None
+        self.G.graph.setdefault("search_params", copy.deepcopy(SEARCH_DEFAULTS))
+        self.G.graph.setdefault("dirty", False)
+        self.G.graph.setdefault("vector_index", {"db_path": "vector_db", "model": DEFAULT_MODEL,
+                                                 "indexed_nodes": 0, "indexed_meta": {}})
+        self._version = 0
+        self._dev_graph: Optional[Tuple[Tuple, DeviceGraph]] = None
+        self._engines: Dict[str, Tuple[Tuple, SearchEngine]] = {}
+
+    # ---- ids ---------------------------------------------------------------------------------
+    @staticmethod
+    def _hash(text: str, length: int = 10) -> str:
+        return _sha(text)[:length]
+
+    @staticmethod
+    def make_entity_id(name: str) -> str:
+        return "ent:" + HierarchicalGraph._hash(name)
+
+    @staticmethod
+    def make_hyperedge_id(uid: str) -> str:
+        return "hedge:" + uid
+
+    @staticmethod
+    def make_summary_id(topic_id: int) -> str:
+        return "sum:%d" % int(topic_id)
+
+    # ---- mutation (ingest-side API the graph builders use) -----------------------------------
+    def _touch(self) -> None:
+        self.G.graph["dirty"] = True
+        self._version += 1
+
+    def add_entity(self, name: str, description: Optional[str] = None, entity_type: Optional[str] = None,
+                   embedding_ref: Optional[Tuple[str, int]] = None,
+                   l1_parents: Optional[Dict[str, float]] = None) -> str:
+        nid = self.name_to_entity_id.get(name)
+        parents_json = json.dumps(l1_parents) if l1_parents else None
+        if nid is None:
+            nid = self.make_entity_id(name)
+            self.G.add_node(nid, node_type="entity", name=name, description=description,
+                            entity_type=entity_type, embedding_ref=embedding_ref, l1_parents=parents_json)
+            self.name_to_entity_id[name] = nid
+        else:
+            attrs = self.G.nodes[nid]
+            if description is not None and not attrs.get("description"):
+                attrs["description"] = description
+            if entity_type is not None and not attrs.get("entity_type"):
+                attrs["entity_type"] = entity_type
+            if embedding_ref is not None:
+                attrs["embedding_ref"] = embedding_ref
+            if l1_parents is not None:
+                attrs["l1_parents"] = json.dumps(l1_parents)
+        self._touch()
+        return nid
+
+    def add_hyperedge(self, uid: str, description: str, relation_type: str,
+                      confidence_score: Optional[float] = None, source_text_ref: Optional[str] = None) -> str:
+        nid = self.make_hyperedge_id(uid)
+        if nid not in self.G:
+            self.G.add_node(nid, node_type="hyperedge", description=description, relation_type=relation_type,
+                            confidence_score=confidence_score, source_text_ref=source_text_ref)
+        self._touch()
+        return nid
+
+    def add_summary(self, topic_id: int, title: Optional[str] = None, summary_text: Optional[str] = None,
+                    confidence: Optional[float] = None, top_words: Optional[List[str]] = None,
+                    members: Optional[List[str]] = None, judge_scores: Optional[Dict[str, Any]] = None,
+                    centroid: Optional[List[float]] = None) -> str:
+        tid = int(topic_id)
+        enc = {"top_words": json.dumps(top_words) if top_words is not None else None,
+               "members": json.dumps(members) if members is not None else None,
+               "judge_scores": json.dumps(judge_scores) if judge_scores is not None else None,
+               "centroid": json.dumps(centroid) if centroid is not None else None}
+        nid = self.topic_to_summary_id.get(tid)
+        if nid is None:
+            nid = self.make_summary_id(tid)
+            # new nodes store falsy lists/dicts as None (the reference's `x if x else None`)
+            self.G.add_node(nid, node_type="summary", topic_id=tid, title=title, summary_text=summary_text,
+                            confidence=confidence,
+                            top_words=enc["top_words"] if top_words else None,
+                            members=enc["members"] if members else None,
+                            judge_scores=enc["judge_scores"] if judge_scores else None,
+                            centroid=enc["centroid"])
+            self.topic_to_summary_id[tid] = nid
+        else:
+            attrs = self.G.nodes[nid]
+            for key, val in (("title", title), ("summary_text", summary_text), ("confidence", confidence)):
+                if val is not None:
+                    attrs[key] = val
+            for key, raw in (("top_words", top_words), ("members", members), ("judge_scores", judge_scores),
+                             ("centroid", centroid)):
+                if raw is not None:
+                    attrs[key] = enc[key]
+        self._touch()
+        return nid
+
+    def add_participation(self, entity_id: str, hyperedge_id: str, role: Optional[str] = None) -> None:
+        self.G.add_edge(entity_id, hyperedge_id, edge_type="participates_in", role=role)
+        self._touch()
+
+    def add_belongs_to(self, entity_id: str, summary_id: str, prob: Optional[float] = None) -> None:
+        self.G.add_edge(entity_id, summary_id, edge_type="belongs_to", prob=prob)
+        self._touch()
+
+    def add_related(self, summary_a: str, summary_b: str, weight: Optional[float] = None,
+                    jaccard: Optional[float] = None, cosine: Optional[float] = None,
+                    overlap: Optional[int] = None, confidence: Optional[float] = None) -> None:
+        self.G.add_edge(summary_a, summary_b, edge_type="related_to", weight=weight, jaccard=jaccard,
+                        cosine=cosine, overlap=overlap, confidence=confidence)
+        self._touch()
+
+    def build_from_artifacts(self, artifacts_dir: str = ARTIFACT_DIR) -> None:
+        raise NotImplementedError("LLM/BERTopic ingest is outside the MI355X retrieval core (SURVEY §2 row 1); "
+                                  "build the graph with the reference pipeline and load() it here")
+
+    def invalidate_device_cache(self) -> None:
+        self._version += 1
+
+    # ---- persistence (node-link JSON, reference :175-236) ------------------------------------
+    def save(self, directory: str = GRAPH_DIR, meta: Optional[Dict[str, Any]] = None) -> None:
+        os.makedirs(directory, exist_ok=True)
+        with open(os.path.join(directory, "structure.json"), "w", encoding="utf-8") as f:
+            json.dump(nx.node_link_data(self.G, edges="links"), f, ensure_ascii=False, indent=2)
+        out = dict(meta or {})
+        out.update({"search_params": self.G.graph.get("search_params", {}),
+                    "graph_hash": self._graph_snapshot_hash(),
+                    "dirty": self.G.graph.get("dirty", False),
+                    "vector_index": self.G.graph.get("vector_index", {})})
+        with open(os.path.join(directory, "meta.json"), "w", encoding="utf-8") as f:
+            json.dump(out, f, ensure_ascii=False, indent=2)
+
+    @classmethod
+    def load(cls, directory: str = GRAPH_DIR) -> "HierarchicalGraph":
+        with open(os.path.join(directory, "structure.json"), encoding="utf-8") as f:
+            data = json.load(f)
+        hg = cls()
+        hg.G = nx.node_link_graph(data, directed=True, edges="links")
+        for nid, attrs in hg.G.nodes(data=True):
+            kind = attrs.get("node_type")
+            if kind == "entity" and attrs.get("name"):
+                hg.name_to_entity_id[attrs["name"]] = nid
+            elif kind == "summary" and attrs.get("topic_id") is not None:
+                hg.topic_to_summary_id[int(attrs["topic_id"])] = nid
+        hg.G.graph.setdefault("search_params", copy.deepcopy(SEARCH_DEFAULTS))
+        hg.G.graph.setdefault("dirty", False)
+        hg.G.graph.setdefault("vector_index", {"db_path": "vector_db", "model": DEFAULT_MODEL,
+                                               "indexed_nodes": 0, "indexed_meta": {}})
+        mp = os.path.join(directory, "meta.json")
+        if os.path.exists(mp):
+            try:
+                with open(mp, encoding="utf-8") as f:
+                    meta = json.load(f)
+                if isinstance(meta.get("search_params"), dict):
+                    hg.G.graph["search_params"] = {**hg.G.graph["search_params"], **meta["search_params"]}
+                if isinstance(meta.get("vector_index"), dict):
+                    hg.G.graph["vector_index"] = meta["vector_index"]
+                if isinstance(meta.get("dirty"), bool):
+                    hg.G.graph["dirty"] = meta["dirty"]
+            except Exception:
+                pass
+        return hg
+
+    def _graph_snapshot_hash(self) -> str:
+        rows = sorted(((nid, d.get("node_type"), d.get("name"), d.get("title"), d.get("summary_text"),
+                        d.get("description")) for nid, d in self.G.nodes(data=True)), key=lambda r: r[0])
+        return _sha(json.dumps(rows, ensure_ascii=False))
+
+    # ---- lookups (reference :426-553) --------------------------------------------------------
+    def get_parents(self, node_id: str) -> List[str]:
+        return list(self.G.successors(node_id))
+
+    def get_children(self, node_id: str) -> List[str]:
+        return list(self.G.predecessors(node_id))
+
+    def find_entity(self, name: str) -> Optional[str]:
+        return self.name_to_entity_id.get(name)
+
+    def find_summary(self, topic_id: int) -> Optional[str]:
+        return self.topic_to_summary_id.get(int(topic_id))
+
+    def _neighbors_by_edge_type(self, node_id: str, direction: str, edge_type: str) -> List[str]:
+        adj = self.G.succ if direction == "out" else self.G.pred
+        return [nb for nb, a in adj[node_id].items() if a.get("edge_type") == edge_type]
+
+    def get_belongs_to(self, node_id: str) -> List[str]:
+        return self._neighbors_by_edge_type(node_id, "out", "belongs_to")
+
+    def get_summary_members(self, summary_id: str) -> List[str]:
+        return self._neighbors_by_edge_type(summary_id, "in", "belongs_to")
+
+    def get_hyperedge_participants(self, hyperedge_id: str) -> List[str]:
+        return self._neighbors_by_edge_type(hyperedge_id, "in", "participates_in")
+
+    def get_entity_hyperedges(self, entity_id: str) -> List[str]:
+        return self._neighbors_by_edge_type(entity_id, "out", "participates_in")
+
+    def get_siblings(self, node_id: str) -> List[str]:
+        sibs = {c for p in set(self.get_belongs_to(node_id)) for c in self.get_summary_members(p)}
+        sibs.discard(node_id)
+        return list(sibs)
+
+    def search_by_name_or_title(self, q: str, limit: int = 20) -> List[Tuple[str, Dict[str, Any]]]:
+        needle = q.lower()
+        hits = []
+        for nid, d in self.G.nodes(data=True):
+            if needle in str(d.get("name") or "").lower() or needle in str(d.get("title") or "").lower():
+                hits.append((nid, d))
+            if len(hits) >= limit:
+                break
+        return hits
+
+    def summaries_with_top_word(self, word: str, limit: int = 50) -> List[str]:
+        w = word.lower()
+        hits: List[str] = []
+        for nid, d in self.G.nodes(data=True):
+            if d.get("node_type") != "summary":
+                continue
+            tw = d.get("top_words")
+            if tw:
+                try:
+                    words = json.loads(tw) if isinstance(tw, str) else tw
+                except Exception:
+                    words = []
+                if any(w in str(x).lower() for x in words):
+                    hits.append(nid)
+            if len(hits) >= limit:
+                break
+        return hits
+
+    def validate_belongs_to_dag(self) -> bool:
+        sub = nx.DiGraph([(u, v) for u, v, a in self.G.edges(data=True) if a.get("edge_type") == "belongs_to"])
+        return nx.is_directed_acyclic_graph(sub)
+
+    def validate_required_attributes(self) -> Dict[str, List[str]]:
+        bad: Dict[str, List[str]] = {"entity": [], "hyperedge": [], "summary": []}
+        for nid, d in self.G.nodes(data=True):
+            kind = d.get("node_type")
+            if kind == "entity" and not d.get("name"):
+                bad["entity"].append(nid)
+            elif kind == "hyperedge" and (not d.get("description") or not d.get("relation_type")):
+                bad["hyperedge"].append(nid)
+            elif kind == "summary" and d.get("topic_id") is None:
+                bad["summary"].append(nid)
+        return bad
+
+    def stats(self) -> Dict[str, Any]:
+        nodes = {k: 0 for k in ("entity", "hyperedge", "summary")}
+        edges = {k: 0 for k in ("participates_in", "belongs_to", "related_to")}
+        for _, d in self.G.nodes(data=True):
+            if d.get("node_type") in nodes:
+                nodes[d["node_type"]] += 1
+        n_edges = 0
+        for _, _, a in self.G.edges(data=True):
+            n_edges += 1
+            if a.get("edge_type") in edges:
+                edges[a["edge_type"]] += 1
+        return {"nodes": nodes, "edges": edges, "n_nodes": self.G.number_of_nodes(), "n_edges": n_edges}
+
+    # ---- vector index (reference :558-673) ---------------------------------------------------
+    def _embedding_text(self, node_id: str) -> Tuple[str, Dict[str, Any]]:
+        d = self.G.nodes[node_id]
+        kind = d.get("node_type")
+        if kind == "entity":
+            text = "Entity: %s. %s" % (d.get("name") or "", d.get("description") or "")
+        elif kind == "summary":
+            words: List[str] = []
+            if d.get("top_words"):
+                try:
+                    words = json.loads(d["top_words"]) if isinstance(d["top_words"], str) else d["top_words"]
+                except Exception:
+                    words = []
+            text = "Summary: %s. %s. Keywords: %s" % (d.get("title") or "",
+                                                      d.get("summary_text") or d.get("summary") or "",
+                                                      ", ".join(words[:10]) if words else "")
+        else:
+            text = "Relation: %s. %s" % (d.get("relation_type") or "", d.get("description") or "")
+        meta = {"node_id": node_id, "node_type": kind,
+                "layer": 0 if kind == "entity" else (1 if kind == "summary" else 0),
+                "judge_overall": parse_judge(d.get("judge_scores")), "confidence": d.get("confidence"),
+                "updated_at": datetime.datetime.utcnow().isoformat() + "Z"}
+        return text, meta
+
+    @staticmethod
+    def _index_key(d: Dict[str, Any]) -> str:
+        return _sha("|".join([str(d.get("node_type")), str(d.get("name") or d.get("title") or ""),
+                              str(d.get("summary_text") or ""), str(d.get("description") or "")]))
+
+    def build_vector_index(self, db_path: str = "vector_db", layers: set = {0, 1}, include_hyperedges: bool = False,
+                           model_name: str = DEFAULT_MODEL, upsert_only: bool = True, reset: bool = False) -> None:
+        os.makedirs(db_path, exist_ok=True)
+        store = VectorStore(db_path)
+        if reset:
+            store.clear()
+        vi = self.G.graph.get("vector_index", {})
+        prev = vi.get("indexed_meta") if isinstance(vi.get("indexed_meta"), dict) else {}
+        todo: List[str] = []
+        for nid, d in self.G.nodes(data=True):
+            kind = d.get("node_type")
+            wanted = (kind == "entity" and 0 in layers) or (kind == "summary" and 1 in layers) or \
+                     (kind == "hyperedge" and include_hyperedges)
+            if wanted and ((not upsert_only) or prev.get(nid) != self._index_key(d)):
+                todo.append(nid)
+        if not todo:
+            return
+        texts, metas = zip(*[self._embedding_text(n) for n in todo])
+        vectors = np.asarray(load_encoder(model_name).encode(list(texts), show_progress_bar=False,
+                                                             normalize_embeddings=True), np.float32)
+        store.upsert(todo, vectors, metas)
+        store.save(model_name)
+        new_meta = dict(prev)
+        for nid in todo:
+            new_meta[nid] = self._index_key(self.G.nodes[nid])
+        self.G.graph["vector_index"] = {"db_path": db_path, "model": model_name,
+                                        "indexed_nodes": len(new_meta), "indexed_meta": new_meta}
+        self.G.graph["dirty"] = False
+
+    # ---- device caches -----------------------------------------------------------------------
+    def _graph_stamp(self) -> Tuple:
+        return (id(self.G), len(self.G), self._version)
+
+    def device_graph(self) -> DeviceGraph:
+        stamp = self._graph_stamp()
+        if self._dev_graph is None or self._dev_graph[0] != stamp:
+            self._dev_graph = (stamp, DeviceGraph(self.G))
+            self._engines.clear()
+        return self._dev_graph[1]
+
+    def search_engine(self, db_path: str) -> SearchEngine:
+        graph = self.device_graph()
+        key = os.path.abspath(db_path)
+        store_stamp = VectorStore.__new__(VectorStore)
+        store_stamp.path = key
+        stamp = store_stamp.stamp()
+        hit = self._engines.get(key)
+        if hit is None or hit[0] != stamp:
+            store = VectorStore(key)
+            n, dim = store.vectors.shape if store.vectors.size else (0, 1)
+            index = DenseIndex(dim, max(n, 1), dtype=os.environ.get("AHR_INDEX_DTYPE", "f32"),
+                               device=graph.device)
+            if n:
+                index.upsert(store.vectors)
+            self._engines[key] = (stamp, SearchEngine(index, store.ids, store.metas, graph))
+        return self._engines[key][1]
+
+    def _encoder(self, model_name: str):
+        if self._query_embedder is None or self._query_embedder_name != model_name:
+            self._query_embedder = load_encoder(model_name)
+            self._query_embedder_name = model_name
+        return self._query_embedder
+
+    # ---- search (reference :675-789) ---------------------------------------------------------
+    def search(self, query: str, top_k: int = 5, member_top_m: int = 5,
+               alpha: Optional[float] = None, beta: Optional[float] = None, gamma: Optional[float] = None,
+               delta: Optional[float] = None, judge_overall_min: Optional[float] = None,
+               confidence_min: Optional[float] = None, type_filter: Optional[List[str]] = None,
+               return_cluster: bool = False, db_path: Optional[str] = None,
+               model_name: Optional[str] = None) -> Any:
+        return self.search_batch([query], top_k, member_top_m, alpha, beta, gamma, delta, judge_overall_min,
+                                 confidence_min, type_filter, return_cluster, db_path, model_name)[0]
+
+    def search_batch(self, queries: Sequence[str], top_k: int = 5, member_top_m: int = 5,
+                     alpha: Optional[float] = None, beta: Optional[float] = None, gamma: Optional[float] = None,
+                     delta: Optional[float] = None, judge_overall_min: Optional[float] = None,
+                     confidence_min: Optional[float] = None, type_filter: Optional[List[str]] = None,
+                     return_cluster: bool = False, db_path: Optional[str] = None,
+                     model_name: Optional[str] = None, query_vectors: Optional[np.ndarray] = None) -> List[Any]:
+        """search() over many queries with one device pass (B = len(queries))."""
+        if top_k > nat.AHR_MAX_K:
+            raise ValueError(f"top_k={top_k} exceeds the fused kernel's limit ({nat.AHR_MAX_K})")
+        params = resolve_search_params(self.G.graph.get("search_params", {}), top_k, member_top_m, alpha, beta,
+                                       gamma, delta, judge_overall_min, confidence_min, type_filter)
+        vi = self.G.graph.get("vector_index") if isinstance(self.G.graph.get("vector_index"), dict) else {}
+        db_path = db_path or vi.get("db_path", "vector_db")
+        model_name = model_name or vi.get("model", DEFAULT_MODEL)
+        engine = self.search_engine(db_path)
+        if query_vectors is None:
+            query_vectors = self._encoder(model_name).encode(list(queries), normalize_embeddings=True)
+        q = torch.from_numpy(np.ascontiguousarray(np.asarray(query_vectors, np.float32)))
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        rows, scores, res = engine.run(q, params)
+        return [self._assemble(engine, rows[b], scores[b], res, b, params.top_k, return_cluster)
+                for b in range(q.shape[0])]
+
+    def _assemble(self, engine: SearchEngine, rows, scores, res, b: int, top_k: int, return_cluster: bool):
+        seeds = []
+        for r, s in zip(rows, scores):
+            if r < 0:
+                continue
+            dist = 1.0 - float(s)  # Chroma's cosine distance of the hit
+            seeds.append({"node_id": engine.row_ids[r], "semantic": 1.0 - float(dist), "meta": engine.row_metas[r]})
+        n_nodes = engine.graph.n_nodes
+        reranked = []
+        for j in range(int(res.out_count[b]) if top_k > 0 else 0):
+            idx = int(res.out_nodes[b, j])
+            nid = engine.node_id(idx)
+            d = self.G.nodes[nid] if nid in self.G else {}
+            kind = d.get("node_type")
+            reranked.append({"node_id": nid, "node_type": kind,
+                             "layer": 0 if kind == "entity" else (1 if kind == "summary" else 0),
+                             "semantic": float(res.out_sem[b, j]), "judge_overall": parse_judge(d.get("judge_scores")),
+                             "confidence": d.get("confidence"), "score": float(res.out_score[b, j]),
+                             "name": d.get("name"), "title": d.get("title")})
+        if not return_cluster:
+            return reranked
+        expanded = []
+        for i in range(int(res.exp_count[b])):
+            idx = int(res.exp_nodes[b, i])
+            nid = engine.node_id(idx)
+            src = int(res.exp_src[b, i])
+            if src >= 0:
+                kind = self.G.nodes[nid].get("node_type") if idx < n_nodes else None
+                expanded.append({**seeds[src], "node_type": kind})
+            else:
+                assumed = nat.NODE_TYPE_NAMES[-1 - src]
+                expanded.append({"node_id": nid, "semantic": float(res.exp_sem[b, i]),
+                                 "meta": {"expanded": True}, "node_type": assumed})
+        return {"seeds": seeds, "expanded": expanded, "reranked": reranked}

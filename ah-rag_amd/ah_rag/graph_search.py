@@ -1,0 +1,274 @@
+"""ah_rag.graph_search — the device graph and the batched search pipeline.
+
+Reference behaviour reproduced (paths relative to Yaron9/AH-RAG):
+  * HierarchicalGraph.search, src/ah_rag/graph/hierarchical_graph.py:675-789: dense top-k of the
+    query against the node index (Chroma query :714), distance -> similarity (:719-724), 1-hop
+    expansion (:726-740), rerank + 4-decimal rounding + stable sort (:742-782), return shapes
+    (:783-789);
+  * GraphEnvironment.expand_{parents,children,related}, src/ah_rag/agent/environment.py:393-480.
+
+Everything after the query embedding runs on the GPU through libahr_hip.so:
+  dense top-k  (ahr_index_query)  ->  row -> node map (one gather)  ->  expansion + rerank
+  (ahr_graph_expand_rerank), batched over B queries, one stream, one host sync per batch.
+The host only turns the small result arrays into the reference's dicts.
+
+DeviceGraph mirrors the networkx graph as per-edge-type CSR lists in the exact order networkx
+iterates neighbours (G.succ / G.pred), so the reference's [:2] / [:member_top_m] truncations and
+the environment's limit/break rules see the same neighbour sequence.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
+
+import networkx as nx
+import numpy as np
+import torch
+
+from . import _native as nat
+
+EDGE_TYPES = ("belongs_to", "related_to", "participates_in")
+# CSR list order of include/ahr.h: belongs_to out/in, related_to out/in, participates_in out/in
+ADJ_SPECS = (("belongs_to", "out"), ("belongs_to", "in"), ("related_to", "out"),
+             ("related_to", "in"), ("participates_in", "out"), ("participates_in", "in"))
+ACTIONS = {"parents": 0, "children": 1, "related": 2}
+
+SEARCH_DEFAULTS = {  # hierarchical_graph.py:37-47
+    "alpha": 0.6, "beta": 0.2, "gamma": 0.1, "delta": 0.1,
+    "judge_overall_min": None, "confidence_min": None, "member_top_m": 5, "type_filter": None,
+    "layer_boost": {"entity": 0.0, "summary": 1.0, "hyperedge": 0.0},
+}
+
+
+def parse_judge(raw: Any) -> Optional[float]:
+    """`overall` of a node's judge_scores (JSON string or dict); None when absent or unparsable."""
+    if not raw:
+        return None
+    try:
+        obj = json.loads(raw) if isinstance(raw, str) else raw
+        return float(obj.get("overall", 0.0))
+    except Exception:
+        return None
+
+
+def _as_float(x: Any) -> float:
+    if x is None:
+        return math.nan
+    try:
+        return float(x)
+    except (TypeError, ValueError):
+        return math.nan
+
+
+class DeviceGraph:
+    """HBM copy of a networkx graph: node attribute table + 6 CSR adjacency lists."""
+
+    def __init__(self, G: nx.DiGraph, device: Optional[torch.device] = None) -> None:
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.ids: List[str] = list(G.nodes)
+        self.index: Dict[str, int] = {nid: i for i, nid in enumerate(self.ids)}
+        n = len(self.ids)
+        self.n_nodes = n
+        self.n_edges = G.number_of_edges()
+        types = np.zeros(n, np.int8)
+        judge = np.full(n, np.nan)
+        conf = np.full(n, np.nan)
+        for i, (nid, d) in enumerate(G.nodes(data=True)):
+            types[i] = nat.NODE_TYPE_CODES.get(d.get("node_type"), nat.NODE_OTHER)
+            j = parse_judge(d.get("judge_scores"))
+            judge[i] = math.nan if j is None else j
+            conf[i] = _as_float(d.get("confidence"))
+        # Rerank terms with the reference's own float64 arithmetic (hierarchical_graph.py:766-767),
+        # so the device score is bit-identical: 1/(1+np.exp(-(judge/10))) and conf/10.
+        with np.errstate(over="ignore", invalid="ignore"):
+            judge_term = np.array([1.0 / (1.0 + np.exp(-((j if j == j else 0.0) / 10.0))) for j in judge])
+        conf_term = np.array([(c / 10.0) if c == c else 0.0 for c in conf])
+        self.node_type = types
+        self.judge = judge
+        self.conf = conf
+        offsets, targets = [], []
+        for etype, direction in ADJ_SPECS:
+            adj = G.succ if direction == "out" else G.pred
+            off = np.zeros(n + 1, np.int64)
+            tgt: List[int] = []
+            for i, nid in enumerate(self.ids):
+                for nb, attrs in adj[nid].items():
+                    if attrs.get("edge_type") == etype:
+                        tgt.append(self.index[nb])
+                off[i + 1] = len(tgt)
+            offsets.append(off)
+            targets.append(np.asarray(tgt, np.int32) if tgt else np.zeros(1, np.int32))
+        self._offsets, self._targets = offsets, targets  # host copies (env LCA / tests)
+        off_ptrs = (nat.ctypes.c_void_p * nat.AHR_ADJ_COUNT)(*[o.ctypes.data for o in offsets])
+        tgt_ptrs = (nat.ctypes.c_void_p * nat.AHR_ADJ_COUNT)(*[t.ctypes.data for t in targets])
+        h = nat.ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_graph_create(
+                n, types.ctypes.data, judge.ctypes.data, conf.ctypes.data, judge_term.ctypes.data,
+                conf_term.ctypes.data, off_ptrs, tgt_ptrs, self.device.index, nat.ctypes.byref(h)),
+                "ahr_graph_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            nat.lib().ahr_graph_destroy(self._h)
+            self._h = nat.ctypes.c_void_p()
+
+    def __del__(self) -> None:
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host helpers over the CSR mirror ------------------------------------------------------
+    def neighbors(self, node: int, adj: int) -> np.ndarray:
+        o = self._offsets[adj]
+        return self._targets[adj][o[node]:o[node + 1]]
+
+    def node_indices(self, ids: Sequence[str]) -> np.ndarray:
+        return np.asarray([self.index.get(x, -1) for x in ids], np.int32)
+
+    # -- device passes -------------------------------------------------------------------------
+    def expand_rerank(self, seed_nodes: torch.Tensor, seed_sem: torch.Tensor, params: "RerankParams",
+                      stream: Optional[torch.cuda.Stream] = None) -> "RerankResult":
+        """seed_nodes int32 [B,k] (-1 absent; >= n_nodes = id unknown to the graph), seed_sem f32 [B,k]."""
+        B, k = seed_nodes.shape
+        dev = self.device
+        fan = max(2, params.member_top_m)
+        max_exp = max(1, k * (1 + fan))
+        top_k = max(params.top_k, 0)
+        kk = max(top_k, 1)
+        en = torch.empty((B, max_exp), dtype=torch.int32, device=dev)
+        es = torch.empty((B, max_exp), dtype=torch.float64, device=dev)
+        ex = torch.empty((B, max_exp), dtype=torch.int32, device=dev)
+        ec = torch.empty((B,), dtype=torch.int32, device=dev)
+        on = torch.empty((B, kk), dtype=torch.int32, device=dev)
+        osem = torch.empty((B, kk), dtype=torch.float64, device=dev)
+        osc = torch.empty((B, kk), dtype=torch.float64, device=dev)
+        oc = torch.empty((B,), dtype=torch.int32, device=dev)
+        c = params.to_c()
+        sn = seed_nodes.to(device=dev, dtype=torch.int32).contiguous()
+        ss = seed_sem.to(device=dev, dtype=torch.float32).contiguous()
+        with torch.cuda.device(dev):
+            nat.check(nat.lib().ahr_graph_expand_rerank(
+                self._h, nat.ptr(sn), nat.ptr(ss), B, k, nat.ctypes.byref(c), max_exp,
+                nat.ptr(en), nat.ptr(es), nat.ptr(ex), nat.ptr(ec), nat.ptr(on), nat.ptr(osem),
+                nat.ptr(osc), nat.ptr(oc), nat.stream_ptr(stream)), "ahr_graph_expand_rerank")
+        return RerankResult(en, es, ex, ec, on, osem, osc, oc)
+
+    def expand(self, action: str, inputs: torch.Tensor, limit: int = 10,
+               stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Batched environment expansion: inputs int32 [B, n_in] node indices (-1 = skip)."""
+        B, n_in = inputs.shape
+        dev = self.device
+        out = torch.empty((B, max(limit, 1)), dtype=torch.int32, device=dev)
+        cnt = torch.empty((B,), dtype=torch.int32, device=dev)
+        x = inputs.to(device=dev, dtype=torch.int32).contiguous()
+        with torch.cuda.device(dev):
+            nat.check(nat.lib().ahr_graph_expand(self._h, ACTIONS[action], nat.ptr(x), B, n_in, int(limit),
+                                                 nat.ptr(out), nat.ptr(cnt), nat.stream_ptr(stream)),
+                      "ahr_graph_expand")
+        return out, cnt
+
+
+@dataclass
+class RerankParams:
+    alpha: float
+    beta: float
+    gamma: float
+    delta: float
+    judge_min: Optional[float]
+    confidence_min: Optional[float]
+    layer_boost: Dict[Any, float]
+    type_filter: Optional[Iterable[str]]
+    member_top_m: int
+    top_k: int
+
+    def to_c(self) -> nat.RerankParams:
+        c = nat.RerankParams()
+        c.alpha, c.beta, c.gamma, c.delta = (float(self.alpha), float(self.beta), float(self.gamma),
+                                            float(self.delta))
+        c.judge_min = math.nan if self.judge_min is None else float(self.judge_min)
+        c.confidence_min = math.nan if self.confidence_min is None else float(self.confidence_min)
+        boost = self.layer_boost or {}
+        c.layer_boost[nat.NODE_OTHER] = float(boost.get(None, 0.0))
+        for name, code in nat.NODE_TYPE_CODES.items():
+            c.layer_boost[code] = float(boost.get(name, 0.0))
+        mask = 0
+        if self.type_filter:
+            for t in self.type_filter:
+                mask |= 1 << nat.NODE_TYPE_CODES.get(t, nat.NODE_OTHER) if t is not None else 1
+        c.type_mask = mask
+        c.member_top_m = int(self.member_top_m)
+        c.top_k = int(max(self.top_k, 0))
+        return c
+
+
+@dataclass
+class RerankResult:
+    exp_nodes: torch.Tensor
+    exp_sem: torch.Tensor
+    exp_src: torch.Tensor
+    exp_count: torch.Tensor
+    out_nodes: torch.Tensor
+    out_sem: torch.Tensor
+    out_score: torch.Tensor
+    out_count: torch.Tensor
+
+    def to_host(self) -> "RerankResult":
+        return RerankResult(*[t.cpu().numpy() for t in (self.exp_nodes, self.exp_sem, self.exp_src,
+                                                        self.exp_count, self.out_nodes, self.out_sem,
+                                                        self.out_score, self.out_count)])
+
+
+def resolve_search_params(stored: Dict[str, Any], top_k: int, member_top_m: Optional[int],
+                          alpha, beta, gamma, delta, judge_overall_min, confidence_min,
+                          type_filter) -> RerankParams:
+    """Argument resolution of hierarchical_graph.py:682-699 (explicit value > graph meta > default)."""
+    sp = {**SEARCH_DEFAULTS, **(stored or {})}
+
+    def pick(v, key):
+        return v if v is not None else sp.get(key)
+
+    if type_filter is None:
+        tf = sp.get("type_filter")
+        type_filter = list(tf) if isinstance(tf, (set, tuple)) else tf
+    return RerankParams(
+        alpha=pick(alpha, "alpha"), beta=pick(beta, "beta"), gamma=pick(gamma, "gamma"),
+        delta=pick(delta, "delta"), judge_min=pick(judge_overall_min, "judge_overall_min"),
+        confidence_min=pick(confidence_min, "confidence_min"),
+        layer_boost=sp.get("layer_boost", SEARCH_DEFAULTS["layer_boost"]), type_filter=type_filter,
+        member_top_m=member_top_m if member_top_m is not None else sp.get("member_top_m", 5),
+        top_k=top_k)
+
+
+class SearchEngine:
+    """DenseIndex (node vectors) + row->node map + DeviceGraph: the batched search pipeline."""
+
+    def __init__(self, index, row_ids: Sequence[str], row_metas: Sequence[Dict[str, Any]],
+                 graph: DeviceGraph) -> None:
+        self.index = index
+        self.row_ids = list(row_ids)
+        self.row_metas = list(row_metas)
+        self.graph = graph
+        n = graph.n_nodes
+        rows = np.asarray([graph.index.get(r, n + i) for i, r in enumerate(self.row_ids)], np.int32)
+        self.row_to_node = torch.from_numpy(rows if len(rows) else np.zeros(1, np.int32)).to(graph.device)
+
+    def node_id(self, idx: int) -> str:
+        n = self.graph.n_nodes
+        return self.graph.ids[idx] if idx < n else self.row_ids[idx - n]
+
+    def run(self, query_vectors: torch.Tensor, params: RerankParams,
+            stream: Optional[torch.cuda.Stream] = None) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
+        """Dense top_k -> expansion -> rerank for a batch. Returns host (rows, scores, result)."""
+        k = max(1, params.top_k)
+        k_dense = min(k, nat.AHR_MAX_K)
+        scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
+        valid = rows >= 0
+        nodes = torch.where(valid, self.row_to_node[rows.clamp_min(0).long()], torch.full_like(rows, -1))
+        res = self.graph.expand_rerank(nodes, scores, params, stream=stream)
+        host = res.to_host()
+        return rows.cpu().numpy(), scores.cpu().numpy(), host
