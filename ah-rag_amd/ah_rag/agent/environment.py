@@ -37,10 +37,13 @@ class GraphEnvironment:
 
     def __init__(self, graph_dir: str = "graph", random_state: int = 42,
                  logging_enabled: bool = True, log_dir: str = "artifacts/phase2", session_id: Optional[str] = None,
-                 debug: bool = False, log_level: str = "normal", redact: bool = True) -> None:
+                 debug: bool = False, log_level: str = "normal", redact: bool = True, *,
+                 graph: Optional[HierarchicalGraph] = None) -> None:
+        """`graph` (keyword-only, not in the reference) shares an already loaded graph, e.g. across
+        the environments of a VecGraphEnvironment, instead of loading graph_dir again."""
         self.graph_dir = graph_dir
         self.random_state = random_state
-        self.hg: Optional[HierarchicalGraph] = None
+        self.hg: Optional[HierarchicalGraph] = graph
         self.last_query: Optional[str] = None
         self.last_results: Optional[Dict[str, Any]] = None
         self.step_count = 0
@@ -301,13 +304,11 @@ class GraphEnvironment:
     # ---- expansions (device kernel) ----------------------------------------------------------
     def _expand(self, action: str, node_ids: List[str], limit: int) -> Tuple[Dict[str, Any], Dict[str, Any]]:
         self._ensure_graph_loaded()
+        ids = expand_batch(self.hg, action, [node_ids], limit)[0]
+        return self._expand_finish(action, node_ids, ids)
+
+    def _expand_finish(self, action: str, node_ids: List[str], ids: List[str]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
         self.step_count += 1
-        dg = self.hg.device_graph()
-        idx = torch.from_numpy(dg.node_indices(node_ids).reshape(1, -1)) if node_ids else \
-            torch.full((1, 1), -1, dtype=torch.int32)
-        out, cnt = dg.expand(action, idx, limit)
-        n = int(cnt[0].item())
-        ids = [dg.ids[i] for i in out[0, :n].tolist()]
         obs = self._observation([{"node_id": x, "semantic": 0.0} for x in ids],
                                 [{"node_id": x, "score": 0.0, "semantic": 0.0} for x in ids])
         info = {"action": "expand_" + action, "inputs": node_ids, "returned": len(ids)}
@@ -345,3 +346,17 @@ class GraphEnvironment:
             pass
         self._log({"action": "end_episode"})
         return summary
+
+
+def expand_batch(hg: HierarchicalGraph, action: str, inputs: Sequence[Sequence[str]], limit: int = 10
+                 ) -> List[List[str]]:
+    """One ahr_graph_expand launch for many environments: inputs[b] are env b's node ids."""
+    dg = hg.device_graph()
+    width = max(1, max((len(x) for x in inputs), default=1))
+    idx = np.full((len(inputs), width), -1, np.int32)
+    for b, ids in enumerate(inputs):
+        if ids:
+            idx[b, :len(ids)] = dg.node_indices(ids)
+    out, cnt = dg.expand(action, torch.from_numpy(idx), limit)
+    out_h, cnt_h = out.cpu().numpy(), cnt.cpu().numpy()
+    return [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] for b in range(len(inputs))]

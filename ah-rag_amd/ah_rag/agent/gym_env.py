@@ -30,8 +30,8 @@ def action_mask(raw_obs: Optional[Dict[str, Any]]) -> List[int]:
 
 class AHRAGGymEnv:
     def __init__(self, graph_dir: str = "graph", max_steps: int = 6, debug: bool = False,
-                 enable_action_mask: bool = True, repeat_penalty: float = 0.02) -> None:
-        self.env = GraphEnvironment(graph_dir=graph_dir, debug=debug, log_level="off", redact=True)
+                 enable_action_mask: bool = True, repeat_penalty: float = 0.02, *, graph=None) -> None:
+        self.env = GraphEnvironment(graph_dir=graph_dir, debug=debug, log_level="off", redact=True, graph=graph)
         self.max_steps = max(1, int(max_steps))
         self._cur_step = 0
         self._last_obs: Optional[Dict[str, Any]] = None

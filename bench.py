@@ -32,6 +32,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from ah_rag.distributed import ShardedDenseIndex, all_gather_keys  # noqa: E402
 from ah_rag.embeddings import DenseIndex, merge_topk_keys  # noqa: E402
 from ah_rag.synthetic import HOTPOT_90K, SYNTH_5M, SyntheticCorpus  # noqa: E402
 
@@ -50,6 +51,8 @@ def parse_args():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--dtype", choices=["bf16", "f16", "f32"], default=None)
     ap.add_argument("--shard", choices=["queries", "rows"], default="queries")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL (default); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=256)
@@ -109,11 +112,15 @@ def main() -> None:
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     spec = HOTPOT_90K if args.workload == "hotpot90k" else SYNTH_5M
     dtype = args.dtype or ("bf16" if args.workload == "hotpot90k" else "f16")
@@ -121,30 +128,32 @@ def main() -> None:
     corpus = SyntheticCorpus(spec, dev)
     rows = corpus.rows()
     N, d = rows.shape
-    if args.shard == "rows" and world > 1:
-        bounds = np.linspace(0, N, world + 1).astype(np.int64)
-        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    sharded = args.shard == "rows" and world > 1
+    if sharded:
+        index = ShardedDenseIndex(d, N, dtype=dtype, device=dev)
+        lo, hi = index.lo, index.hi
+        for s0 in range(0, N, 1_000_000):
+            index.upsert_global(s0, rows[s0:min(N, s0 + 1_000_000)])
+        local = index.local
     else:
         lo, hi = 0, N
-    index = DenseIndex(d, hi - lo, dtype=dtype, device=dev)
-    for s in range(lo, hi, 1_000_000):
-        index.upsert(rows[s:min(hi, s + 1_000_000)], start=s - lo)
+        index = local = DenseIndex(d, N, dtype=dtype, device=dev)
+        for s0 in range(0, N, 1_000_000):
+            local.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
     salt = rank if args.shard == "queries" else 0
     q, src = corpus.queries(B, rows, salt=salt)
     index.reserve(B, k)
     scores = torch.empty((B, k), dtype=torch.float32, device=dev)
     out_rows = torch.empty((B, k), dtype=torch.int32, device=dev)
     keys = torch.empty((B, k), dtype=torch.int64, device=dev)
-    gathered = torch.empty((world, B, k), dtype=torch.int64, device=dev) if world > 1 else None
-    sharded = args.shard == "rows" and world > 1
 
     def step():
         if sharded:
-            index.query_keys(q, k, row_base=lo, out=keys)
-            dist.all_gather_into_tensor(gathered, keys)
-            s_, r_, _ = merge_topk_keys(gathered.permute(1, 0, 2), k)
+            index.query_keys(q, k, out=keys)
+            gathered = all_gather_keys(keys)                  # RCCL all-gather over xGMI
+            s_, r_, _ = merge_topk_keys(gathered.permute(1, 0, 2).contiguous(), k)
             return s_, r_
-        index.query(q, k, out=(scores, out_rows))
+        local.query(q, k, out=(scores, out_rows))
         return scores, out_rows
 
     for _ in range(args.warmup):
@@ -153,7 +162,7 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    index.profile_begin(args.steps)
+    local.profile_begin(args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -162,7 +171,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    prof = index.profile_end()
+    prof = local.profile_end()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -198,7 +207,7 @@ def main() -> None:
         peak = MFMA_PEAK_TFLOPS[dtype]
         elem = 4 if dtype == "f32" else 2
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
-        plan = index.plan(B)
+        plan = local.plan(B)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
