@@ -110,6 +110,19 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// Workgroup barrier that waits for this wave's LDS traffic but leaves global_load_lds in flight
+// (__syncthreads() would emit vmcnt(0) and drain the ring).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int DT>
 __device__ __forceinline__ void mfma_step(const u32x4& a, const u32x4& b, f32x16& acc) {
   if constexpr (DT == DT_BF16) {
@@ -144,7 +157,7 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) 
 }
 
 enum { MODE_TOPK = 0, MODE_GROUPMAX = 1 };
-enum { kFlagXcdRemap = 1, kFlagSkipEpilogue = 2 };  // kFlagSkipEpilogue: ablation only (wrong output)
+enum { kFlagXcdRemap = 1, kFlagSkipEpilogue = 2, kFlagUseRing = 4 };  // 2, 4: ablation only
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
 //             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
@@ -200,29 +213,28 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
   }
   if (tid < 2) flag[tid] = 0;
 
-  // Staging map: thread t moves chunk (t & 7) of rows (t >> 3) + 32 i, i = 0..3, of both the
-  // corpus tile and the query tile: each wave instruction reads 8 full 128-B row segments.
-  const int st_row = tid >> 3;
-  const int st_ch = tid & 7;
-  const uint8_t* gB = queries + ((int64_t)q0 + st_row) * row_stride + st_ch * 16;
+  // Staging by global_load_lds (no staging registers): wave w fills rows [32w, 32w+32) of both
+  // tiles, 8 rows (1 KiB) per instruction; lane l lands at (row 8j + l/8, physical chunk l%8) and
+  // therefore loads logical chunk (l%8) ^ swz(row): the XOR swizzle moves to the source address.
+  const int ld_row = lane >> 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   int round_id = 0;
 
   for (int t = t_begin; t < t_end; ++t) {
     const int64_t r0 = (int64_t)t * kTileRows;
-    const uint8_t* gA = corpus + (r0 + st_row) * row_stride + st_ch * 16;
-    u32x4 stA[4], stB[4];
+    auto stage = [&](int kt, unsigned char* buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      stA[i] = *reinterpret_cast<const u32x4*>(gA + (int64_t)(32 * i) * row_stride);
-      stB[i] = *reinterpret_cast<const u32x4*>(gB + (int64_t)(32 * i) * row_stride);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = st_row + 32 * i;
-      *reinterpret_cast<u32x4*>(smem + kOffBuf0 + swz(row, st_ch)) = stA[i];
-      *reinterpret_cast<u32x4*>(smem + kOffBuf0 + kTileRows * kRowBytes + swz(row, st_ch)) = stB[i];
-    }
-    __syncthreads();
+      for (int j = 0; j < 4; ++j) {
+        const int row = wave_u * 32 + 8 * j + ld_row;
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int64_t goff = (int64_t)row * row_stride + kt * kRowBytes + c * 16;
+        glds16(corpus + r0 * row_stride + goff, buf + (wave_u * 32 + 8 * j) * kRowBytes);
+        glds16(queries + (int64_t)q0 * row_stride + goff, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
+      }
+    };
+    stage(0, smem + kOffBuf0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -233,42 +245,42 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
         for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
 
     for (int kt = 0; kt < n_ktiles; ++kt) {
-      const bool more = kt + 1 < n_ktiles;
-      if (more) {
-        const int64_t off = (int64_t)(kt + 1) * kRowBytes;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          stA[i] = *reinterpret_cast<const u32x4*>(gA + (int64_t)(32 * i) * row_stride + off);
-          stB[i] = *reinterpret_cast<const u32x4*>(gB + (int64_t)(32 * i) * row_stride + off);
-        }
-      }
+      if (kt + 1 < n_ktiles) stage(kt + 1, smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0));
       const unsigned char* buf = smem + ((kt & 1) ? kOffBuf1 : kOffBuf0);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      // Two fragment register sets, order pinned with sched_barrier: the LDS reads of step g+1
+      // are in flight while the MFMAs of step g run.
+      u32x4 fa0[2], fb0[2], fa1[2], fb1[2];
+      auto frag_load = [&](int g, u32x4 (&a)[2], u32x4 (&b)[2]) {
         const int ch = 2 * g + fh;
-        u32x4 a[2], b[2];
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
           a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj)
-          b[bj] = *reinterpret_cast<const u32x4*>(buf + kTileRows * kRowBytes +
-                                                   swz(wq * 64 + bj * 32 + fr, ch));
+          b[bj] = *reinterpret_cast<const u32x4*>(buf + kTileRows * kRowBytes + swz(wq * 64 + bj * 32 + fr, ch));
+      };
+      auto frag_mma = [&](const u32x4 (&a)[2], const u32x4 (&b)[2]) {
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
           for (int bj = 0; bj < 2; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
-      }
-      if (more) {
-        unsigned char* nb = smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = st_row + 32 * i;
-          *reinterpret_cast<u32x4*>(nb + swz(row, st_ch)) = stA[i];
-          *reinterpret_cast<u32x4*>(nb + kTileRows * kRowBytes + swz(row, st_ch)) = stB[i];
-        }
-      }
-      __syncthreads();
+      };
+      frag_load(0, fa0, fb0);
+      frag_load(1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_load(2, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_load(3, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa1, fb1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 landed (this wave's part)
+      lds_barrier();                                    // ... everyone's; everyone done with kt
     }
 
     if constexpr (MODE == MODE_GROUPMAX) {
@@ -428,6 +440,269 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
   }
 
   if (MODE == MODE_TOPK && tid < kTileQ && q0 + tid < n_q) {
+    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j)
+      if (j < k_out) dst[j] = L[j];
+  }
+}
+
+// =============================================================================================
+// v2: the same tile and epilogue, with the K-loop fed by a 3-stage global_load_lds ring.
+// Loads run two k-tiles ahead (counted vmcnt, raw s_barrier: nothing drains the ring) and the
+// prefetch crosses corpus-tile boundaries, so the epilogue of tile t overlaps the loads of tile
+// t+1. The epilogue therefore has LDS of its own; the ~155 KiB total allows one workgroup per CU
+// (4 waves, one per SIMD) — the regime where an in-flight staging pipeline pays (guide §5).
+// =============================================================================================
+namespace ring {
+constexpr int kStages = 3;
+constexpr int kStageBytes = kBufBytes;                     // A tile + B tile of one k-tile, 32 KiB
+constexpr int kProdCap = 6;
+constexpr int kOffCand = kStages * kStageBytes;            // 96 KiB
+constexpr int kCandBytes = kTileQ * 4 * kProdCap * 8;      // 24 KiB
+constexpr int kOffScratch = kOffCand + kCandBytes;
+constexpr int kScratchBytes = 4 * 64 * 32 * 4;             // 32 KiB
+constexpr int kOffThrKey = kOffScratch + kScratchBytes;
+constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
+constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
+constexpr int kOffFlag = kOffCnt + kTileQ * 4 * 4;
+constexpr int kLdsBytes = kOffFlag + 16;
+static_assert(kLdsBytes <= 160 * 1024, "ring kernel LDS exceeds 160 KiB");
+static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
+}  // namespace ring
+
+template <int DT, int KCAP>
+__global__ __launch_bounds__(kThreads, 1) void topk_ring_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
+    int n_rows, int n_q, int n_ktiles, int tiles_per_split, int n_row_tiles, uint32_t row_base,
+    int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
+    int qblocks, int flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1;
+  const int wq = wave & 1;
+  const int fr = lane & 31;
+  const int fh = lane >> 5;
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q0 = qb * kTileQ;
+  const int t_begin = split * tiles_per_split;
+  const int t_end = min(t_begin + tiles_per_split, n_row_tiles);
+  const int total = t_end > t_begin ? (t_end - t_begin) * n_ktiles : 0;
+
+  uint64_t* thr_key = reinterpret_cast<uint64_t*>(smem + ring::kOffThrKey);
+  float* thr_score = reinterpret_cast<float*>(smem + ring::kOffThrScore);
+  int* cnt = reinterpret_cast<int*>(smem + ring::kOffCnt);
+  int* flag = reinterpret_cast<int*>(smem + ring::kOffFlag);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + ring::kOffCand);
+  float* scr = reinterpret_cast<float*>(smem + ring::kOffScratch) + wave * 64 * 32;
+
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  if (tid < kTileQ) {
+    const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
+    thr_score[tid] = seed;
+    thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
+  }
+  if (tid < 2) flag[tid] = 0;
+
+  // glds map: wave w fills rows [32w, 32w+32) of both tiles, 8 rows (1 KiB) per instruction;
+  // lane l lands at LDS slot (row 8j + l/8, physical chunk l%8) and so loads logical chunk
+  // (l%8) ^ swz(row) from global: the XOR swizzle moves to the source address.
+  const int ld_row = lane >> 3;
+  auto issue = [&](int s) {
+    const int t = t_begin + s / n_ktiles;
+    const int kt = s - (s / n_ktiles) * n_ktiles;
+    unsigned char* buf = smem + (s % ring::kStages) * ring::kStageBytes;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wave * 32 + 8 * j + ld_row;
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int64_t goff = (int64_t)row * row_stride + kt * kRowBytes + c * 16;
+      glds16(corpus + (int64_t)t * kTileRows * row_stride + goff, buf + (wave * 32 + 8 * j) * kRowBytes);
+      glds16(queries + (int64_t)q0 * row_stride + goff,
+             buf + kTileRows * kRowBytes + (wave * 32 + 8 * j) * kRowBytes);
+    }
+  };
+  if (total > 0) issue(0);
+  if (total > 1) issue(1);
+  __syncthreads();  // thresholds visible (nothing in flight can be drained harmfully here? the two
+                    // prologue stages are: this costs one wait at start only)
+
+  f32x16 acc[2][2];
+  int round_id = 0;
+  for (int s = 0; s < total; ++s) {
+    if (s + 1 < total) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage s landed; s+1 may still fly
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();  // every wave's stage-s data visible; every wave done with stage s-1
+    if (s + 2 < total) issue(s + 2);  // refills the buffer stage s-1 used
+    const int tk = s / n_ktiles;
+    const int kt = s - tk * n_ktiles;
+    if (kt == 0) {
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
+    }
+    const unsigned char* buf = smem + (s % ring::kStages) * ring::kStageBytes;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = 2 * g + fh;
+      u32x4 a[2], b[2];
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+        a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+        b[bj] = *reinterpret_cast<const u32x4*>(buf + kTileRows * kRowBytes + swz(wq * 64 + bj * 32 + fr, ch));
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
+    }
+    if (kt != n_ktiles - 1) continue;
+
+    // ---- epilogue of corpus tile (t_begin + tk); the next tile's first stages are in flight
+    const int64_t r0 = (int64_t)(t_begin + tk) * kTileRows;
+    if (flags & kFlagSkipEpilogue) {
+      float sink = 0.f;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
+      if (sink == 1234.5678f) part_keys[0] = 1;
+      continue;
+    }
+    uint64_t consumed = 0;
+    const int pid = wr * 2 + fh;
+    for (;;) {
+      ++round_id;
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        const int ql = wq * 64 + bj * 32 + fr;
+        const float ths = (q0 + ql < n_q) ? thr_score[ql] : INFINITY;
+        const uint64_t thk = thr_key[ql];
+        float m = acc[0][bj][0];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[bi][bj][r]);
+        int c = 0;
+        uint64_t flagged = __ballot(m >= ths);
+        if (flagged) {
+          if (m >= ths) {
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+              for (int c4 = 0; c4 < 4; ++c4) {
+                f32x4 v4 = {acc[bi][bj][4 * c4], acc[bi][bj][4 * c4 + 1], acc[bi][bj][4 * c4 + 2],
+                            acc[bi][bj][4 * c4 + 3]};
+                *reinterpret_cast<f32x4*>(scr + lane * 32 + bi * 16 + 4 * c4) = v4;
+              }
+          }
+          __builtin_amdgcn_wave_barrier();
+          const uint32_t cons_bj = (uint32_t)(consumed >> (bj * 32));
+          const uint32_t thk_lo = (uint32_t)thk, thk_hi = (uint32_t)(thk >> 32);
+          const int v = lane & 31;
+          const int row_v = (v >> 4) * 32 + (v & 3) + 8 * ((v >> 2) & 3);
+          while (flagged) {
+            const int fA = __builtin_ctzll(flagged);
+            flagged &= flagged - 1;
+            const int fB = flagged ? __builtin_ctzll(flagged) : fA;
+            const bool hasB = flagged != 0;
+            if (hasB) flagged &= flagged - 1;
+            const bool upper = lane >= 32;
+            const bool active = !upper || hasB;
+            const int f = upper ? fB : fA;
+            const float tsA = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fA));
+            const float tsB = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fB));
+            const uint64_t tkA = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fA) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fA);
+            const uint64_t tkB = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fB) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fB);
+            const uint32_t csA = (uint32_t)__builtin_amdgcn_readlane((int)cons_bj, fA);
+            const uint32_t csB = (uint32_t)__builtin_amdgcn_readlane((int)cons_bj, fB);
+            const int cA = __builtin_amdgcn_readlane(c, fA);
+            const int cB = __builtin_amdgcn_readlane(c, fB);
+            const float ts = upper ? tsB : tsA;
+            const uint64_t tk = upper ? tkB : tkA;
+            const uint32_t cs = upper ? csB : csA;
+            const int cf = upper ? cB : cA;
+            const float val = scr[f * 32 + v];
+            const int row = (int)r0 + wr * 64 + 4 * (f >> 5) + row_v;
+            bool pass = active && val >= ts && !((cs >> v) & 1u) && row < n_rows;
+            uint64_t key = 0;
+            if (pass) {
+              key = make_key(val, row_base + (uint32_t)row);
+              pass = key > tk;
+            }
+            const uint64_t bal = __ballot(pass);
+            const uint32_t half = upper ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+            const int rank = __builtin_popcount(half & ((1u << v) - 1u));
+            const bool store = pass && cf + rank < ring::kProdCap;
+            if (store) {
+              const int qf = wq * 64 + bj * 32 + (f & 31);
+              const int pf = wr * 2 + (f >> 5);
+              cand[(qf * 4 + pf) * ring::kProdCap + cf + rank] = key;
+            }
+            const uint64_t sbal = __ballot(store);
+            const int totA = __builtin_popcount((uint32_t)bal);
+            const int totB = __builtin_popcount((uint32_t)(bal >> 32));
+            if (cA + totA > ring::kProdCap || (hasB && cB + totB > ring::kProdCap)) flag[round_id & 1] = round_id;
+            if (lane == fA) {
+              c = min(cA + totA, ring::kProdCap);
+              consumed |= (uint64_t)(uint32_t)sbal << (bj * 32);
+            }
+            if (hasB && lane == fB) {
+              c = min(cB + totB, ring::kProdCap);
+              consumed |= (uint64_t)(uint32_t)(sbal >> 32) << (bj * 32);
+            }
+          }
+        }
+        cnt[ql * 4 + pid] = c;
+      }
+      lds_barrier();
+      if (tid < kTileQ) {
+        bool changed = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int n = cnt[tid * 4 + u];
+          const uint64_t* src = cand + (tid * 4 + u) * ring::kProdCap;
+          for (int i = 0; i < n; ++i) list_insert<KCAP>(L, src[i]);
+          changed |= n > 0;
+        }
+        if (changed) {
+          const uint64_t kth = list_at<KCAP>(L, k_out - 1);
+          if (kth > thr_key[tid]) {
+            thr_key[tid] = kth;
+            thr_score[tid] = key_score(kth);
+          }
+        }
+      }
+      lds_barrier();
+      if (flag[round_id & 1] != round_id) break;
+    }
+  }
+
+  if (tid < kTileQ && q0 + tid < n_q) {
     uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
 #pragma unroll
     for (int j = 0; j < KCAP; ++j)
@@ -719,13 +994,17 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 struct SearchPlan {
   int qblocks, n_row_tiles, n_splits, tiles_per_split;
   bool xcd_remap;
+  bool ring;
 };
 
-// Resident workgroups of the tile kernel per CU (VGPR-limited to 2 waves/SIMD, 4-wave groups).
-constexpr int kResidentSlots = 256 * 2;
+// Resident workgroups: v1 tile kernel 2 per CU (VGPR/LDS limited), ring kernel 1 per CU.
+constexpr int kResidentSlotsV1 = 256 * 2;
+constexpr int kResidentSlotsRing = 256;
 
 SearchPlan plan_search(const ahr_index* ix, int B) {
   SearchPlan p;
+  p.ring = (ix->debug_flags & kFlagUseRing) != 0;
+  const int kResidentSlots = p.ring ? kResidentSlotsRing : kResidentSlotsV1;
   p.qblocks = (int)cdiv(B, kTileQ);
   p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
   // One wave of workgroups that fills every resident slot; splits padded to a multiple of 8
@@ -752,7 +1031,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
   }
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
   const int64_t qblocks = cdiv(B, kTileQ);
-  const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlots, qblocks)), 8) * 8;
+  const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlotsV1, qblocks)), 8) * 8;
   const int64_t p_need = (int64_t)B * std::max<int64_t>(max_splits, kSampleMax / kTileRows) * k;
   if (p_need > ix->part_cap) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
@@ -791,6 +1070,21 @@ void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_s
                      n_splits, qblocks, flags);
 }
 
+template <int DT, int KCAP>
+void launch_ring(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                 const float* thr, int flags, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_ring_kernel<DT, KCAP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, ring::kLdsBytes);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((topk_ring_kernel<DT, KCAP>), dim3((unsigned)(p.n_splits * p.qblocks)), dim3(kThreads),
+                     ring::kLdsBytes, s, ix->rows, ix->qbuf, ix->row_stride, n_rows, B,
+                     ix->d_pad * ix->elem / kRowBytes, p.tiles_per_split, p.n_row_tiles, row_base, k, ix->part,
+                     thr, p.n_splits, p.qblocks, flags);
+}
+
 template <int DT>
 void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base,
                    hipStream_t s) {
@@ -810,6 +1104,14 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
+  if (p.ring) {
+    switch (kcap_for(k)) {
+      case 8: launch_ring<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s); break;
+      case 16: launch_ring<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s); break;
+      default: launch_ring<DT, 32>(ix, p, n, B, k, row_base, thr, flags, s); break;
+    }
+    return;
+  }
   switch (kcap_for(k)) {
     case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
     case 16: launch_tile<DT, 16, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
@@ -1054,7 +1356,7 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  ix->debug_flags = flags & kFlagSkipEpilogue;
+  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagUseRing);
   return AHR_OK;
 }
 

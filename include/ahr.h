@@ -99,8 +99,8 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_c
 /* Rows scored by the threshold pre-pass (0 disables it; else a power of two in [128, 1024]). */
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
-/* Ablation switches for profiling (2 = skip the top-k epilogue: GEMM cost only, results are
- * garbage). Never set in production. */
+/* Ablation switches for profiling: 2 = skip the top-k epilogue (GEMM cost only, results are
+ * garbage); 4 = use the glds-ring tile kernel (correct, slower on MI355X). Never set in production. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
 /* Launch geometry the next query of batch B would use (diagnostics / bench reporting). */

@@ -50,8 +50,8 @@ def main():
         q, _ = c.queries(B, rows)
         res = {}
         for r in range(a.rounds):
-            for name, sample, flags in (("prod", 8192, 0), ("s4096", 4096, 0), ("s16384", 16384, 0),
-                                        ("no_prepass", 0, 0), ("gemm_only", 0, 2)):
+            for name, sample, flags in (("prod", 8192, 0), ("ring", 8192, 4), ("no_prepass", 0, 0),
+                                        ("gemm_only", 0, 2), ("ring_gemm_only", 0, 6)):
                 ix.set_sample_rows(sample)
                 ix.set_debug_flags(flags)
                 t = run(ix, q, a.k, a.steps)

@@ -1,0 +1,95 @@
+"""Summarise rocprofv3 PMC passes (tools/profile_pmc.sh output) into profiles/pmc_traffic.json.
+
+Per kernel and per launch (mean over launches):
+  * HBM read bytes  = FETCH_SIZE (KiB) x 1024 x 2   — gfx950 FETCH_SIZE reports half the bytes of
+    wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md §HBM); our corpus and query
+    staging loads are exactly that pattern;
+  * HBM write bytes = WRITE_SIZE (KiB) x 1024       — exact for 16-B stores; our partial-list stores
+    are 8 B/lane (uncalibrated width, reported as measured);
+  * MFMA work from SQ_INSTS_VALU_MFMA_MOPS_BF16 and the kernel duration from the kernel trace.
+Infinity-Cache hits are counted inside FETCH_SIZE (the counter sits on the L2's memory side), so
+"HBM" here means "beyond L2".
+
+Usage: python tools/pmc_summary.py gpurun_out/pmc5 [--out profiles/pmc_traffic.json]
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+
+def _rows(pattern: str):
+    files = glob.glob(pattern)
+    if not files:
+        return []
+    with open(files[0], newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def _short(name: str) -> str:
+    m = re.search(r"ahr::(?:dense|graph)::(\w+)(<[^>]*>)?", name)
+    if not m:
+        return name[:60]
+    return m.group(1) + (m.group(2) or "")
+
+
+def counters(pattern: str):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in _rows(pattern):
+        agg[_short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def durations(pattern: str):
+    out = {}
+    for r in _rows(pattern):
+        out[_short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmc_dir")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    fetch = counters(os.path.join(a.pmc_dir, "fetch", "*", "*_counter_collection.csv"))
+    write = counters(os.path.join(a.pmc_dir, "write", "*", "*_counter_collection.csv"))
+    sq = counters(os.path.join(a.pmc_dir, "sq", "*", "*_counter_collection.csv"))
+    dur = durations(os.path.join(a.pmc_dir, "trace", "*", "*_kernel_stats.csv"))
+    out = {"_method": ("FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction) + WRITE_SIZE KiB x 1024, "
+                       "mean per launch, separate rocprofv3 --pmc passes; durations from --kernel-trace --stats"),
+           "_source": a.pmc_dir}
+    for k in sorted(set(fetch) | set(write) | set(dur)):
+        base = k.split("<")[0]
+        if base not in ("topk_tile_kernel", "topk_ring_kernel", "merge_lane_lists_kernel", "merge_heads_kernel",
+                        "merge_kernel", "sample_kth_kernel", "convert_rows_kernel", "expand_rerank_kernel",
+                        "expand_kernel"):
+            continue
+        rec = out.setdefault(base, {"variants": {}})
+        f = fetch.get(k, {}).get("FETCH_SIZE", [])
+        w = write.get(k, {}).get("WRITE_SIZE", [])
+        mf = sq.get(k, {}).get("SQ_INSTS_VALU_MFMA_MOPS_BF16", [])
+        v = {"launches": len(f) or len(w),
+             "read_bytes_per_launch": (sum(f) / len(f)) * 1024 * 2 if f else None,
+             "write_bytes_per_launch": (sum(w) / len(w)) * 1024 if w else None,
+             "mfma_mops_bf16_per_launch": (sum(mf) / len(mf)) if mf else None,
+             "avg_us_trace": dur.get(k, {}).get("avg_us")}
+        if v["read_bytes_per_launch"] is not None and v["write_bytes_per_launch"] is not None:
+            v["hbm_bytes_per_launch"] = v["read_bytes_per_launch"] + v["write_bytes_per_launch"]
+        rec["variants"][k] = v
+        best = max(rec["variants"].values(), key=lambda x: x.get("avg_us_trace") or 0)
+        rec["hbm_bytes_per_launch"] = best.get("hbm_bytes_per_launch")
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in out.items() if not k.startswith("_")}))
+
+
+if __name__ == "__main__":
+    main()
