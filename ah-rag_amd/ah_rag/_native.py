@@ -97,7 +97,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_index_profile_begin": ([_P, _I], _I),
         "ahr_index_profile_end": ([_P, _P, _P], _I),
         "ahr_index_set_sample_rows": ([_P, _I], _I),
-        "ahr_index_plan": ([_P, _I, _P, _P, _P], _I),
+        "ahr_index_plan": ([_P, _I, _I, _P, _P, _P, _P], _I),
         "ahr_index_set_debug_flags": ([_P, _I], _I),
         "ahr_index_query": ([_P, _P, _I, _I, _I, _P, _P, _P], _I),
         "ahr_index_query_keys": ([_P, _P, _I, _I, _I, _L, _P, _P], _I),

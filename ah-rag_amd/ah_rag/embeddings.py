@@ -199,14 +199,19 @@ class DenseIndex:
         nat.check(nat.lib().ahr_index_set_sample_rows(self._h, int(rows)), "ahr_index_set_sample_rows")
 
     def set_debug_flags(self, flags: int) -> None:
-        """Ablation switches (2 = skip the top-k epilogue; results become garbage)."""
+        """Ablation switches (2 = skip the top-k epilogue, results become garbage; 4 = ring kernel;
+        8 = never the wide kernel)."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
-    def plan(self, batch: int) -> dict:
-        a, b, c = nat.ctypes.c_int(), nat.ctypes.c_int(), nat.ctypes.c_int()
-        nat.check(nat.lib().ahr_index_plan(self._h, int(batch), nat.ctypes.byref(a), nat.ctypes.byref(b),
-                                           nat.ctypes.byref(c)), "ahr_index_plan")
-        return {"n_splits": a.value, "tiles_per_split": b.value, "qblocks": c.value}
+    _KERNELS = ("tile128", "ring128", "wide256")
+
+    def plan(self, batch: int, k: int = 10) -> dict:
+        """Launch geometry of a query of this batch size and top-k (diagnostics)."""
+        kern, a, b, c = (nat.ctypes.c_int() for _ in range(4))
+        nat.check(nat.lib().ahr_index_plan(self._h, int(batch), int(k), nat.ctypes.byref(kern), nat.ctypes.byref(a),
+                                           nat.ctypes.byref(b), nat.ctypes.byref(c)), "ahr_index_plan")
+        return {"kernel": self._KERNELS[kern.value], "n_splits": a.value, "tiles_per_split": b.value,
+                "qblocks": c.value}
 
     def profile_begin(self, max_calls: int) -> None:
         """Record HIP events around each query stage for the next max_calls calls."""

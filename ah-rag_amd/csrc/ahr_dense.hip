@@ -6,7 +6,7 @@
 // (what Chroma returns when its HNSW is exhaustive), batched over B queries.
 //
 // Data layout in HBM (owned by ahr_index):
-//   corpus  [cap_pad][d_pad] row-major, dtype bf16 | f16 | f32, cap_pad % 128 == 0,
+//   corpus  [cap_pad][d_pad] row-major, dtype bf16 | f16 | f32, cap_pad % 256 == 0,
 //           rows 16-B aligned, zero padding dim..d_pad. fp32 rows are stored with each group
 //           of 8 lanes permuted to (evens | odds) so one 16-B LDS read feeds four consecutive
 //           v_mfma_f32_32x32x2_f32 k-steps (see frag_f32 below).
@@ -115,6 +115,19 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// LDS-DMA through a buffer descriptor (MUBUF `buffer_load ... lds`). Unlike the FLAT-encoded
+// global_load_lds, LLVM does not count it as a possibly out-of-order LDS access, so the
+// fragment reads that follow keep counted lgkmcnt(N) waits. The descriptor covers one tile
+// (32-bit offsets, whatever the corpus size) and must be built from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
+                                           0, 0);
+}
+
 // Workgroup barrier that waits for this wave's LDS traffic but leaves global_load_lds in flight
 // (__syncthreads() would emit vmcnt(0) and drain the ring).
 __device__ __forceinline__ void lds_barrier() {
@@ -157,7 +170,8 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) 
 }
 
 enum { MODE_TOPK = 0, MODE_GROUPMAX = 1 };
-enum { kFlagXcdRemap = 1, kFlagSkipEpilogue = 2, kFlagUseRing = 4 };  // 2, 4: ablation only
+enum { kFlagXcdRemap = 1, kFlagSkipEpilogue = 2, kFlagUseRing = 4, kFlagNoWide = 8, kFlagWideStages4 = 16 };
+// 2, 4, 8, 16: ablation only
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
 //             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
@@ -710,6 +724,317 @@ __global__ __launch_bounds__(kThreads, 1) void topk_ring_kernel(
   }
 }
 
+// =============================================================================================
+// wide: 256-row x 256-query workgroup tile (8 waves of 64 rows x 128 queries), one workgroup per
+// CU. A 128x128 tile needs 32 KiB of operands per 64-deep K-step for 2 MFLOP (64 FLOP/B): at
+// ~950 TFLOP/s that is ~58 GB/s per CU from L2, the per-CU L2 delivery the guide measures
+// (66-73 GB/s), so the tile shape, not MFMA issue, capped v1. 256x256 is 128 FLOP/B.
+// Operands stream through a 3-stage global_load_lds ring of 32-deep K-steps (64 B per row), kept
+// in flight across corpus tiles and across the epilogue (the epilogue's LDS is separate). The
+// epilogue screens flagged producer lanes two at a time through a 256-B per-wave scratch and
+// reserves slots of a per-query candidate buffer with one LDS atomic per flagged lane.
+// =============================================================================================
+namespace wide {
+constexpr int kThreads = 512;
+constexpr int kTileRows = 256;
+constexpr int kTileQ = 256;
+constexpr int kRowBytes = 64;  // one k-tile of one row: 4 chunks of 16 B
+constexpr int kStageBytes = (kTileRows + kTileQ) * kRowBytes;  // 32 KiB
+
+// LDS map for a ring of STAGES slots (STAGES - 1 k-tiles in flight). The candidate buffer
+// shrinks as the ring grows so both fit in 160 KiB.
+template <int STAGES>
+struct Layout {
+  static constexpr int kSlots = STAGES >= 4 ? 8 : 16;            // candidates per query per round
+  static constexpr int kOffCand = STAGES * kStageBytes;
+  static constexpr int kCandBytes = kTileQ * kSlots * 8;
+  static constexpr int kOffScratch = kOffCand + kCandBytes;
+  static constexpr int kScratchBytes = 8 * 64 * 4;               // per wave: 2 lanes x 32 scores
+  static constexpr int kOffThrKey = kOffScratch + kScratchBytes;
+  static constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
+  static constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
+  static constexpr int kOffFlag = kOffCnt + kTileQ * 4;
+  static constexpr int kLdsBytes = kOffFlag + 16;
+  static_assert(kLdsBytes <= 160 * 1024, "wide kernel LDS exceeds 160 KiB");
+  static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
+};
+
+// 64-B rows: a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the row so the 16
+// rows of a ds_read_b128 lane group ({0-3,12-15,20-27} / {4-11,16-19,28-31}) hit 16 distinct
+// 16-B slots.
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * kRowBytes + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+}  // namespace wide
+
+template <int DT, int KCAP, int STAGES>
+__global__ __launch_bounds__(wide::kThreads, 1) void topk_wide_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
+    int n_rows, int n_q, int n_ktiles, int n_splits, int n_row_tiles, uint32_t row_base, int k_out,
+    uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int qblocks, int flags) {
+  using LY = wide::Layout<STAGES>;
+  using wide::kRowBytes;
+  using wide::kStageBytes;
+  using wide::swz;
+  constexpr int kSlots = LY::kSlots;
+  constexpr int kStages = STAGES;
+  constexpr int TR = wide::kTileRows;
+  constexpr int TQ = wide::kTileQ;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave & 3;   // 64-row quarter of the tile
+  const int wq = wave >> 2;  // 128-query half of the block
+  const int fr = lane & 31;
+  const int fh = lane >> 5;
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q0 = qb * TQ;
+  // Contiguous, balanced tile ranges (sizes differ by at most one tile).
+  const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
+  const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
+  const int total = (t_end - t_begin) * n_ktiles;
+
+  uint64_t* thr_key = reinterpret_cast<uint64_t*>(smem + LY::kOffThrKey);
+  float* thr_score = reinterpret_cast<float*>(smem + LY::kOffThrScore);
+  int* cnt = reinterpret_cast<int*>(smem + LY::kOffCnt);
+  int* flag = reinterpret_cast<int*>(smem + LY::kOffFlag);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + LY::kOffCand);
+  float* scr = reinterpret_cast<float*>(smem + LY::kOffScratch) + wave * 64;
+
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  if (tid < TQ) {
+    const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
+    thr_score[tid] = seed;
+    thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
+    cnt[tid] = 0;
+  }
+  if (tid < 2) flag[tid] = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init read retired before the ring counts
+
+  // glds map: wave w fills rows [32w, 32w+32) of the corpus tile and of the query tile, 16 rows
+  // (1 KiB) per instruction; lane l lands at (row 16j + l/4, physical chunk l%4) and loads the
+  // logical chunk (l%4) ^ swz(row) from global memory.
+  const int ld_row = lane >> 2;
+  const uint32_t tile_bytes = (uint32_t)(TR * row_stride);
+  const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, tile_bytes);
+  uint32_t ld_off[2];  // this lane's byte offset inside a tile, k-tile 0
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = wave * 32 + 16 * j + ld_row;
+    ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 3) ^ ((row >> 2) & 3)) << 4);
+  }
+  auto issue = [&](int s) {
+    const int t = t_begin + s / n_ktiles;
+    const int kt = s - (s / n_ktiles) * n_ktiles;
+    unsigned char* buf = smem + (s % kStages) * kStageBytes;
+    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)t * TR * row_stride, tile_bytes);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t off = ld_off[j] + kt * kRowBytes;
+      blds16(c_rsrc, off, buf + (wave * 32 + 16 * j) * kRowBytes);
+      blds16(q_rsrc, off, buf + TR * kRowBytes + (wave * 32 + 16 * j) * kRowBytes);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < STAGES - 1; ++i)
+    if (i < total) issue(i);
+
+  f32x16 acc[2][4];
+  int round_id = 0;
+  for (int s = 0; s < total; ++s) {
+    // stage s landed: the 4 loads per later stage already issued (up to STAGES - 2) may fly
+    if constexpr (STAGES >= 4) {
+      if (s + 2 < total) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else if (s + 1 < total) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      if (s + 1 < total) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    lds_barrier();  // every wave's stage-s data visible; every wave done reading stage s-1
+    if (s + STAGES - 1 < total) issue(s + STAGES - 1);  // refills the slot stage s-1 used
+    const int tk = s / n_ktiles;
+    const int kt = s - tk * n_ktiles;
+    if (kt == 0) {
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
+    }
+    const unsigned char* buf = smem + (s % kStages) * kStageBytes;
+    u32x4 fa0[2], fb0[4], fa1[2], fb1[4];
+    auto frag_load = [&](int g, u32x4 (&a)[2], u32x4 (&b)[4]) {
+      const int ch = 2 * g + fh;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+        a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj)
+        b[bj] = *reinterpret_cast<const u32x4*>(buf + TR * kRowBytes + swz(wq * 128 + bj * 32 + fr, ch));
+    };
+    auto frag_mma = [&](const u32x4 (&a)[2], const u32x4 (&b)[4]) {
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
+    };
+    frag_load(0, fa0, fb0);
+    frag_load(1, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    frag_mma(fa0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    frag_mma(fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt != n_ktiles - 1) continue;
+
+    // ---- epilogue of corpus tile (t_begin + tk); the next tile's first stages are in flight.
+    const int64_t r0 = (int64_t)(t_begin + tk) * TR;
+    if (flags & kFlagSkipEpilogue) {
+      float sink = 0.f;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
+      if (sink == 1234.5678f) part_keys[0] = 1;
+      continue;
+    }
+    // Each query's 256 tile scores sit in 8 producer lanes (4 row-waves x 2 lane halves), 32
+    // registers each. consumed[bj] bit v: score v of column bj already handed over this tile.
+    uint32_t consumed[4] = {0u, 0u, 0u, 0u};
+    const int v = lane & 31;
+    const int row_v = (v >> 4) * 32 + (v & 3) + 8 * ((v >> 2) & 3);
+    const bool upper = lane >= 32;
+    for (;;) {
+      ++round_id;
+#pragma unroll
+      for (int bj = 0; bj < 4; ++bj) {
+        const int ql = wq * 128 + bj * 32 + fr;
+        const float ths = (q0 + ql < n_q) ? thr_score[ql] : INFINITY;
+        const uint64_t thk = thr_key[ql];
+        float m0 = acc[0][bj][0], m1 = acc[0][bj][1], m2 = acc[1][bj][0], m3 = acc[1][bj][1];
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+          m0 = fmaxf(m0, acc[0][bj][r]);
+          m1 = fmaxf(m1, acc[0][bj][r + 1]);
+          m2 = fmaxf(m2, acc[1][bj][r]);
+          m3 = fmaxf(m3, acc[1][bj][r + 1]);
+        }
+        const float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+        uint64_t flagged = __ballot(m >= ths);
+        if (!flagged) continue;
+        const uint32_t thk_lo = (uint32_t)thk, thk_hi = (uint32_t)(thk >> 32);
+        while (flagged) {
+          const int fA = __builtin_ctzll(flagged);
+          flagged &= flagged - 1;
+          const bool hasB = flagged != 0;
+          const int fB = hasB ? __builtin_ctzll(flagged) : fA;
+          if (hasB) flagged &= flagged - 1;
+          // the two flagged lanes publish their 32 scores: A -> scr[0..31], B -> scr[32..63]
+          if (lane == fA || (hasB && lane == fB)) {
+            float* dst = scr + (lane == fA ? 0 : 32);
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+              for (int c4 = 0; c4 < 4; ++c4) {
+                f32x4 v4 = {acc[bi][bj][4 * c4], acc[bi][bj][4 * c4 + 1], acc[bi][bj][4 * c4 + 2],
+                            acc[bi][bj][4 * c4 + 3]};
+                *reinterpret_cast<f32x4*>(dst + bi * 16 + 4 * c4) = v4;
+              }
+          }
+          __builtin_amdgcn_wave_barrier();
+          const int f = upper ? fB : fA;
+          // readlane needs a wave-uniform lane: read both flagged lanes' state, then select
+          const float tsA = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fA));
+          const float tsB = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fB));
+          const float ts = upper ? tsB : tsA;
+          const uint64_t tk64 = upper
+              ? (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fB) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fB))
+              : (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fA) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fA));
+          const uint32_t csA = (uint32_t)__builtin_amdgcn_readlane((int)consumed[bj], fA);
+          const uint32_t csB = (uint32_t)__builtin_amdgcn_readlane((int)consumed[bj], fB);
+          const uint32_t cs = upper ? csB : csA;
+          const float val = scr[lane];
+          const int row = (int)r0 + wr * 64 + 4 * (f >> 5) + row_v;
+          bool pass = (!upper || hasB) && val >= ts && !((cs >> v) & 1u) && row < n_rows;
+          uint64_t key = 0;
+          if (pass) {
+            key = make_key(val, row_base + (uint32_t)row);
+            pass = key > tk64;
+          }
+          const uint64_t bal = __ballot(pass);
+          const int totA = __builtin_popcount((uint32_t)bal);
+          const int totB = __builtin_popcount((uint32_t)(bal >> 32));
+          const int qA = wq * 128 + bj * 32 + (fA & 31);
+          const int qB = wq * 128 + bj * 32 + (fB & 31);
+          // slot reservation: one LDS atomic per flagged lane (lanes 0 and 32)
+          int got = 0;
+          if (v == 0) {
+            const int tot = upper ? totB : totA;
+            if (tot) got = atomicAdd(&cnt[upper ? qB : qA], tot);
+          }
+          const int baseA = __builtin_amdgcn_readlane(got, 0);
+          const int baseB = __builtin_amdgcn_readlane(got, 32);
+          const uint32_t half = upper ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+          const int rank = __builtin_popcount(half & ((1u << v) - 1u));
+          const int base = upper ? baseB : baseA;
+          const bool store = pass && base + rank < kSlots;
+          if (store) cand[(upper ? qB : qA) * kSlots + base + rank] = key;
+          const uint64_t sbal = __ballot(store);
+          if (baseA + totA > kSlots || (hasB && baseB + totB > kSlots)) flag[round_id & 1] = round_id;
+          if (lane == fA) consumed[bj] |= (uint32_t)sbal;
+          if (hasB && lane == fB) consumed[bj] |= (uint32_t)(sbal >> 32);
+        }
+      }
+      lds_barrier();
+      if (tid < TQ) {
+        const int n = min(cnt[tid], kSlots);
+        if (n > 0) {
+          for (int i = 0; i < n; ++i) list_insert<KCAP>(L, cand[tid * kSlots + i]);
+          const uint64_t kth = list_at<KCAP>(L, k_out - 1);
+          if (kth > thr_key[tid]) {
+            thr_key[tid] = kth;
+            thr_score[tid] = key_score(kth);
+          }
+          cnt[tid] = 0;
+        }
+      }
+      lds_barrier();
+      // parity slots: a round-R overflow write never races a slower wave's read of round R-1
+      if (flag[round_id & 1] != round_id) break;
+    }
+  }
+
+  if (tid < TQ && q0 + tid < n_q) {
+    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j)
+      if (j < k_out) dst[j] = L[j];
+  }
+}
+
 // Merge n_lists sorted key lists per query into the top k. One wave per query: every lane
 // folds a strided share into a register list, then k rounds of a wave-wide max pick winners.
 template <int KCAP>
@@ -766,7 +1091,8 @@ __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict_
     // count over the wave with ballots: scalar popcounts, no cross-lane data movement
     int c = 0;
 #pragma unroll
-    for (int j = 0; j < kGroupMax / 64; ++j) c += __builtin_popcountll(__ballot(v[j] >= cand));
+    for (int j = 0; j < kGroupMax / 64; ++j)
+      if (64 * j < S) c += __builtin_popcountll(__ballot(v[j] >= cand));  // S is wave-uniform
     if (c >= k) ans = cand;
   }
   if (lane == 0) thr[q] = unord_f32(ans);
@@ -952,7 +1278,7 @@ struct ahr_index {
   int64_t count = 0;
   uint8_t* rows = nullptr;
   uint8_t* qbuf = nullptr;
-  int64_t q_cap = 0;  // rows in qbuf (multiple of 128)
+  int64_t q_cap = 0;  // rows in qbuf (multiple of kRowPad)
   uint64_t* part = nullptr;
   int64_t part_cap = 0;  // uint64 elements
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
@@ -991,20 +1317,45 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
     (void)hipEventRecord(ix->prof_events[(size_t)ix->prof_calls * (kStages + 1) + stage], s);
 }
 
+enum { KERNEL_V1 = 0, KERNEL_RING = 1, KERNEL_WIDE = 2 };
+
 struct SearchPlan {
+  int kernel;
   int qblocks, n_row_tiles, n_splits, tiles_per_split;
   bool xcd_remap;
-  bool ring;
 };
+
+// Corpus and query buffers are padded to whole 256-row tiles (the wide kernel's tile).
+constexpr int64_t kRowPad = 256;
+// Below this batch the 256-query tile wastes MFMA work on padding; v1's 128 is used instead.
+constexpr int kWideMinBatch = 512;
 
 // Resident workgroups: v1 tile kernel 2 per CU (VGPR/LDS limited), ring kernel 1 per CU.
 constexpr int kResidentSlotsV1 = 256 * 2;
 constexpr int kResidentSlotsRing = 256;
 
-SearchPlan plan_search(const ahr_index* ix, int B) {
+SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
-  p.ring = (ix->debug_flags & kFlagUseRing) != 0;
-  const int kResidentSlots = p.ring ? kResidentSlotsRing : kResidentSlotsV1;
+  if (ix->debug_flags & kFlagUseRing) {
+    p.kernel = KERNEL_RING;
+  } else if (kcap_for(k) <= 16 && B >= kWideMinBatch && !(ix->debug_flags & kFlagNoWide)) {
+    p.kernel = KERNEL_WIDE;
+  } else {
+    p.kernel = KERNEL_V1;
+  }
+  if (p.kernel == KERNEL_WIDE) {
+    // One workgroup per CU; splits a multiple of 8 (rounded down: a 257th workgroup would run
+    // as a second wave) so the XCD remap keeps a split's query blocks on one XCD.
+    p.qblocks = (int)cdiv(B, wide::kTileQ);
+    p.n_row_tiles = (int)cdiv(ix->count, wide::kTileRows);
+    int want = std::max(1, 256 / p.qblocks);
+    want = std::min(want, std::max(1, p.n_row_tiles));
+    p.xcd_remap = want >= 8;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    return p;
+  }
+  const int kResidentSlots = p.kernel == KERNEL_RING ? kResidentSlotsRing : kResidentSlotsV1;
   p.qblocks = (int)cdiv(B, kTileQ);
   p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
   // One wave of workgroups that fills every resident slot; splits padded to a multiple of 8
@@ -1019,7 +1370,7 @@ SearchPlan plan_search(const ahr_index* ix, int B) {
 }
 
 int ensure_query_ws(ahr_index* ix, int B, int k) {
-  const int64_t q_need = cdiv(B, kTileQ) * kTileQ;
+  const int64_t q_need = cdiv(B, kRowPad) * kRowPad;
   if (q_need > ix->q_cap) {
     if (ix->qbuf) AHR_HIP(hipFree(ix->qbuf));
     ix->qbuf = nullptr;
@@ -1032,7 +1383,9 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
   const int64_t qblocks = cdiv(B, kTileQ);
   const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlotsV1, qblocks)), 8) * 8;
-  const int64_t p_need = (int64_t)B * std::max<int64_t>(max_splits, kSampleMax / kTileRows) * k;
+  const int64_t wide_splits = std::max<int64_t>(1, 256 / cdiv(B, wide::kTileQ));  // >= plan's
+  const int64_t p_need =
+      (int64_t)B * std::max<int64_t>(std::max(max_splits, wide_splits), kSampleMax / kTileRows) * k;
   if (p_need > ix->part_cap) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
     ix->part = nullptr;
@@ -1085,6 +1438,22 @@ void launch_ring(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
                      thr, p.n_splits, p.qblocks, flags);
 }
 
+template <int DT, int KCAP, int STAGES>
+void launch_wide(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                 const float* thr, int flags, hipStream_t s) {
+  constexpr int lds = wide::Layout<STAGES>::kLdsBytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_wide_kernel<DT, KCAP, STAGES>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((topk_wide_kernel<DT, KCAP, STAGES>), dim3((unsigned)(p.n_splits * p.qblocks)),
+                     dim3(wide::kThreads), lds, s, ix->rows, ix->qbuf, ix->row_stride, n_rows, B,
+                     ix->d_pad * ix->elem / wide::kRowBytes, p.n_splits, p.n_row_tiles, row_base, k, ix->part,
+                     thr, p.qblocks, flags);
+}
+
 template <int DT>
 void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base,
                    hipStream_t s) {
@@ -1096,7 +1465,7 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     float* scores = ix->sample;
     float* t = ix->sample + (int64_t)B * (S / 16);
     const int G = S / 16;  // 16-row groups
-    launch_tile<DT, 8, MODE_GROUPMAX>(ix, S / kTileRows, p.qblocks, 1, S / kTileRows, S, B, k, 0,
+    launch_tile<DT, 8, MODE_GROUPMAX>(ix, S / kTileRows, (int)cdiv(B, kTileQ), 1, S / kTileRows, S, B, k, 0,
                                       nullptr, scores, G, 0, s);
     hipLaunchKernelGGL(sample_kth_kernel, dim3(B), dim3(64), 0, s, scores, G, k, t);
     thr = t;
@@ -1104,7 +1473,18 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
-  if (p.ring) {
+  if (p.kernel == KERNEL_WIDE) {
+    const bool deep = (flags & kFlagWideStages4) == 0;  // 4 stages by default; flag 16 = 3 stages
+    if (kcap_for(k) == 8) {
+      if (deep) launch_wide<DT, 8, 4>(ix, p, n, B, k, row_base, thr, flags, s);
+      else launch_wide<DT, 8, 3>(ix, p, n, B, k, row_base, thr, flags, s);
+    } else {
+      if (deep) launch_wide<DT, 16, 4>(ix, p, n, B, k, row_base, thr, flags, s);
+      else launch_wide<DT, 16, 3>(ix, p, n, B, k, row_base, thr, flags, s);
+    }
+    return;
+  }
+  if (p.kernel == KERNEL_RING) {
     switch (kcap_for(k)) {
       case 8: launch_ring<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s); break;
       case 16: launch_ring<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s); break;
@@ -1165,7 +1545,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
                      (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                      ix->row_stride, ix->d_pad, ix->dtype);
-  SearchPlan p = plan_search(ix, B);
+  SearchPlan p = plan_search(ix, B, k);
   if (ix->count > 0) {
     switch (ix->dtype) {
       case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, s); break;
@@ -1203,7 +1583,7 @@ int ahr_index_create(int dim, int dtype, int64_t capacity, int device, ahr_index
   ix->d_pad = (int)cdiv(dim, lanes_per_ktile) * lanes_per_ktile;
   ix->device = device;
   ix->capacity = capacity;
-  ix->cap_pad = std::max<int64_t>(kTileRows, cdiv(capacity, kTileRows) * kTileRows);
+  ix->cap_pad = std::max<int64_t>(kRowPad, cdiv(capacity, kRowPad) * kRowPad);
   ix->row_stride = (int64_t)ix->d_pad * ix->elem;
   if (hipMalloc(&ix->rows, ix->cap_pad * ix->row_stride) != hipSuccess) {
     delete ix;
@@ -1356,13 +1736,15 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagUseRing);
+  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagUseRing | kFlagNoWide | kFlagWideStages4);
   return AHR_OK;
 }
 
-int ahr_index_plan(const ahr_index* ix, int B, int* n_splits, int* tiles_per_split, int* qblocks) {
-  if (!ix || B <= 0) return fail(AHR_EINVAL, "bad plan request");
-  SearchPlan p = plan_search(ix, B);
+int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
+                   int* qblocks) {
+  if (!ix || B <= 0 || k <= 0 || k > AHR_MAX_K) return fail(AHR_EINVAL, "bad plan request");
+  SearchPlan p = plan_search(ix, B, k);
+  if (kernel) *kernel = p.kernel;
   if (n_splits) *n_splits = p.n_splits;
   if (tiles_per_split) *tiles_per_split = p.tiles_per_split;
   if (qblocks) *qblocks = p.qblocks;

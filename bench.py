@@ -207,7 +207,7 @@ def main() -> None:
         peak = MFMA_PEAK_TFLOPS[dtype]
         elem = 4 if dtype == "f32" else 2
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
-        plan = local.plan(B)
+        plan = local.plan(B, k)
         out = {
             "metric": METRIC,
             "value": round(value, 1),

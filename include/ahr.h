@@ -100,11 +100,14 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_c
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
 /* Ablation switches for profiling: 2 = skip the top-k epilogue (GEMM cost only, results are
- * garbage); 4 = use the glds-ring tile kernel (correct, slower on MI355X). Never set in production. */
+ * garbage); 4 = use the 128x128 glds-ring tile kernel; 8 = never use the 256x256 wide kernel;
+ * 16 = wide kernel with a 3-stage ring (4, 8 and 16 give correct results). Never set in production. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
-/* Launch geometry the next query of batch B would use (diagnostics / bench reporting). */
-int ahr_index_plan(const ahr_index* ix, int B, int* n_splits, int* tiles_per_split, int* qblocks);
+/* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
+ * *kernel: 0 = 128x128 tile kernel, 1 = 128x128 glds-ring kernel, 2 = 256x256 wide kernel. */
+int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
+                   int* qblocks);
 
 /* Pre-size the per-query workspace so ahr_index_query() allocates nothing (graph-capturable). */
 int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k);

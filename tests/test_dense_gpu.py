@@ -184,3 +184,60 @@ def test_many_lists_merge(cuda):
     es, er = dr.topk(C, Q, 32, mode="fma")
     np.testing.assert_array_equal(r, er)
     np.testing.assert_array_equal(s, es.astype(np.float32))
+
+
+# ---- 256x256 wide kernel (B >= 512, k <= 16) --------------------------------------------------
+
+@pytest.mark.parametrize("n,d,B,k", [(12000, 384, 700, 10), (3001, 256, 1500, 16), (5000, 768, 513, 5)])
+def test_wide_f32_bit_exact(cuda, n, d, B, k):
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(2000 + n + B)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype="f32", device=cuda)
+    assert ix.plan(B, k)["kernel"] == "wide256"
+    ix.close()
+    s, r = _run("f32", C, Q, k, cuda)
+    es, er = dr.topk(C, Q, k, mode="fma")
+    np.testing.assert_array_equal(r, er)
+    np.testing.assert_array_equal(s, es.astype(np.float32))
+
+
+@pytest.mark.parametrize("k,sample", [(10, 8192), (16, 8192), (5, 0), (10, 0), (1, 8192)])
+def test_wide_equals_tile128(cuda, k, sample):
+    """Both kernels chain the same 16-deep MFMA steps in k order: bitwise equal results. Sample 0
+    (no pre-pass) starts every tile with 256 candidates per query: exercises overflow rounds."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(31 + k + sample)
+    C = _clustered(rng, 70001, 768)
+    Q = _clustered(rng, 1030, 768)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ix.set_sample_rows(sample)
+    assert ix.plan(len(Q), k)["kernel"] == "wide256"
+    a = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(8)
+    assert ix.plan(len(Q), k)["kernel"] == "tile128"
+    b = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(16)  # wide kernel with the 3-stage ring / 16-slot candidate buffer
+    c = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.close()
+    for x in (b, c):
+        np.testing.assert_array_equal(a[1], x[1])
+        np.testing.assert_array_equal(a[0], x[0])
+
+
+def test_wide_ties_order_by_row(cuda):
+    """Duplicate corpus rows tie exactly: lower row id first, across tiles and splits."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(12)
+    base = _clustered(rng, 300, 256)
+    C = np.concatenate([base] * 40)  # 12000 rows, each vector 40 times
+    Q = base[rng.integers(0, 300, 600)]
+    ix = DenseIndex(256, len(C), dtype="f32", device=cuda)
+    ix.upsert(C)
+    s, r = [t.cpu().numpy() for t in ix.query(Q, 16)]
+    ix.close()
+    es, er = dr.topk(C, Q, 16, mode="fma")
+    np.testing.assert_array_equal(r, er)
+    np.testing.assert_array_equal(s, es.astype(np.float32))

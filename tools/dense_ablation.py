@@ -1,7 +1,9 @@
 """Ablation timings of the dense search stages on one GPU (interleaved variants, one process).
 
-Variants: production; no threshold pre-pass; GEMM only (epilogue skipped, wrong output).
-Prints per-stage milliseconds (HIP events on the query stream) per variant and batch size.
+Variants (--variants name:sample_rows:debug_flags,...): production; pre-pass sample sizes;
+no threshold pre-pass (sample 0); GEMM only (flag 2: epilogue skipped, wrong output); the
+glds-ring kernel (flag 4). Prints per-stage milliseconds (HIP events on the query stream; an
+empty stage reads ~5 us) per variant and batch size.
 """
 import argparse
 import json
@@ -37,6 +39,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="prod:8192:0,v1:8192:8,no_prepass:0:0,gemm_only:0:2,v1_gemm_only:0:10")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     spec = HOTPOT_90K if a.workload == "hotpot90k" else SYNTH_5M
@@ -45,13 +48,13 @@ def main():
     ix = DenseIndex(rows.shape[1], rows.shape[0], dtype=a.dtype, device=dev)
     for s in range(0, rows.shape[0], 1_000_000):
         ix.upsert(rows[s:s + 1_000_000], start=s)
+    variants = [(n, int(sr), int(fl)) for n, sr, fl in (v.split(":") for v in a.variants.split(","))]
     out = []
     for B in [int(x) for x in a.batches.split(",")]:
         q, _ = c.queries(B, rows)
         res = {}
         for r in range(a.rounds):
-            for name, sample, flags in (("prod", 8192, 0), ("ring", 8192, 4), ("no_prepass", 0, 0),
-                                        ("gemm_only", 0, 2), ("ring_gemm_only", 0, 6)):
+            for name, sample, flags in variants:
                 ix.set_sample_rows(sample)
                 ix.set_debug_flags(flags)
                 t = run(ix, q, a.k, a.steps)
@@ -60,7 +63,7 @@ def main():
         ix.set_debug_flags(0)
         best = {n: min(v, key=lambda d: sum(d.values())) for n, v in res.items()}
         flops = 2.0 * B * rows.shape[0] * rows.shape[1]
-        line = {"B": B, "plan": ix.plan(B)}
+        line = {"B": B, "plan": ix.plan(B, a.k)}
         for n, t in best.items():
             line[n] = t
             line[n + "_tile_TFs"] = round(flops / (t["tile_topk"] * 1e-3) / 1e12, 1)
