@@ -199,11 +199,11 @@ class DenseIndex:
         nat.check(nat.lib().ahr_index_set_sample_rows(self._h, int(rows)), "ahr_index_set_sample_rows")
 
     def set_debug_flags(self, flags: int) -> None:
-        """Ablation switches (2 = skip the top-k epilogue, results become garbage; 4 = ring kernel;
-        8 = never the wide kernel)."""
+        """Ablation switches (include/ahr.h): 2 = skip the top-k epilogue (garbage results),
+        8 = 128x128 tile kernel, 64 = 256x128 lane kernel, 256 = group maxima only (garbage)."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
-    _KERNELS = ("tile128", "ring128", "wide256")
+    _KERNELS = ("tile128", "lane256", "lane256x128")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

@@ -13,14 +13,21 @@
 //   queries [q_cap][d_pad] same format, converted from fp32 on every call.
 //   partial keys [B][n_splits][k] uint64 (ahr_common.h key format), merged by merge_kernel.
 //
-// Kernel (topk_tile_kernel): one workgroup = 4 waves (2 along rows x 2 along queries) owns a
-// 128-query block and a contiguous range of 128-row corpus tiles. Per tile it runs a K-loop of
-// 32x32 MFMAs with the corpus tile as the A operand and the query tile as B, so every lane's
-// accumulator column is ONE query and its 16 registers are 16 corpus rows of it. The score
-// tile is never stored: the epilogue compares it with the per-query k-th best key held in
-// LDS, appends the survivors to per-query LDS candidate lists, and one owner thread per query
-// folds them into a register top-k list (sorted, capacity KCAP). Survivors become rare after
-// the first tile, so the epilogue costs a compare per score.
+// Kernels (both keep the score tile in MFMA accumulators, never in memory; corpus rows are the
+// A operand and queries the B operand of 32x32 MFMAs, so each lane's accumulator column is ONE
+// query and its registers are corpus rows of it):
+//  * topk_lane_kernel (default for B >= 512, k <= 16): a workgroup of 8 waves owns a 256-query
+//    block and a contiguous range of 256-row corpus tiles; each wave covers all 256 rows for its
+//    32 queries, so every lane keeps its query's partial top-k list in registers and screens its
+//    own scores (16-row group maxima against its threshold, scan of the rare passing groups):
+//    no candidate buffers, atomics or barriers in the epilogue. Operands stream through a
+//    4-stage buffer LDS-DMA ring. The two half-wave lists merge at the end.
+//  * topk_tile_kernel (small batches, k > 16, and the threshold pre-pass): 4 waves (2 along rows
+//    x 2 along queries), 128-query block x 128-row tiles, two workgroups per CU; survivors are
+//    screened cooperatively into per-query LDS candidate lists that one owner thread per query
+//    folds into its register top-k list.
+// The pre-pass (first 8192 rows, 16-row group maxima, k-th largest per query) seeds every
+// query's threshold with a valid lower bound of its final k-th best score.
 #include "ahr_common.h"
 #include "ahr.h"
 
@@ -170,8 +177,15 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) 
 }
 
 enum { MODE_TOPK = 0, MODE_GROUPMAX = 1 };
-enum { kFlagXcdRemap = 1, kFlagSkipEpilogue = 2, kFlagUseRing = 4, kFlagNoWide = 8, kFlagWideStages4 = 16 };
-// 2, 4, 8, 16: ablation only
+enum {
+  kFlagXcdRemap = 1,
+  kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
+  kFlagTile128 = 8,       // always the 128x128 tile kernel
+  kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
+  kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
+};
+constexpr int kKernelFlags = kFlagTile128 | kFlagLane256q128;
+// every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
 //             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
@@ -462,301 +476,32 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
 }
 
 // =============================================================================================
-// v2: the same tile and epilogue, with the K-loop fed by a 3-stage global_load_lds ring.
-// Loads run two k-tiles ahead (counted vmcnt, raw s_barrier: nothing drains the ring) and the
-// prefetch crosses corpus-tile boundaries, so the epilogue of tile t overlaps the loads of tile
-// t+1. The epilogue therefore has LDS of its own; the ~155 KiB total allows one workgroup per CU
-// (4 waves, one per SIMD) — the regime where an in-flight staging pipeline pays (guide §5).
+// lane kernel: every wave covers ALL rows of the workgroup's corpus tile for its own 32 queries
+// (MFMA 32x32: the corpus rows are the A operand, NB row blocks; the wave's 32 queries are B),
+// so each lane's accumulator column is one query and the lane keeps that query's partial top-k
+// list in registers. The epilogue is then lane-local: per 16-row group a max and a compare with
+// the lane's threshold; only groups that reach it are scanned and inserted. No LDS candidate
+// buffers, atomics or barriers, so nothing in the epilogue waits on another wave, and with two
+// workgroups per CU one workgroup's epilogue runs beside the other's MFMAs. The two half-wave
+// lists of a query (lanes l and l+32 hold disjoint rows) are merged once, at the end.
+// Operands stream through a buffer LDS-DMA ring of 32-deep K-steps (64 B per row).
 // =============================================================================================
-namespace ring {
-constexpr int kStages = 3;
-constexpr int kStageBytes = kBufBytes;                     // A tile + B tile of one k-tile, 32 KiB
-constexpr int kProdCap = 6;
-constexpr int kOffCand = kStages * kStageBytes;            // 96 KiB
-constexpr int kCandBytes = kTileQ * 4 * kProdCap * 8;      // 24 KiB
-constexpr int kOffScratch = kOffCand + kCandBytes;
-constexpr int kScratchBytes = 4 * 64 * 32 * 4;             // 32 KiB
-constexpr int kOffThrKey = kOffScratch + kScratchBytes;
-constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
-constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
-constexpr int kOffFlag = kOffCnt + kTileQ * 4 * 4;
-constexpr int kLdsBytes = kOffFlag + 16;
-static_assert(kLdsBytes <= 160 * 1024, "ring kernel LDS exceeds 160 KiB");
-static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
-}  // namespace ring
-
-template <int DT, int KCAP>
-__global__ __launch_bounds__(kThreads, 1) void topk_ring_kernel(
-    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
-    int n_rows, int n_q, int n_ktiles, int tiles_per_split, int n_row_tiles, uint32_t row_base,
-    int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
-    int qblocks, int flags) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1;
-  const int wq = wave & 1;
-  const int fr = lane & 31;
-  const int fh = lane >> 5;
-  int split, qb;
-  if (flags & kFlagXcdRemap) {
-    const int x = blockIdx.x & 7;
-    const int i = blockIdx.x >> 3;
-    split = (i / qblocks) * 8 + x;
-    qb = i % qblocks;
-  } else {
-    split = blockIdx.x % n_splits;
-    qb = blockIdx.x / n_splits;
-  }
-  const int q0 = qb * kTileQ;
-  const int t_begin = split * tiles_per_split;
-  const int t_end = min(t_begin + tiles_per_split, n_row_tiles);
-  const int total = t_end > t_begin ? (t_end - t_begin) * n_ktiles : 0;
-
-  uint64_t* thr_key = reinterpret_cast<uint64_t*>(smem + ring::kOffThrKey);
-  float* thr_score = reinterpret_cast<float*>(smem + ring::kOffThrScore);
-  int* cnt = reinterpret_cast<int*>(smem + ring::kOffCnt);
-  int* flag = reinterpret_cast<int*>(smem + ring::kOffFlag);
-  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + ring::kOffCand);
-  float* scr = reinterpret_cast<float*>(smem + ring::kOffScratch) + wave * 64 * 32;
-
-  uint64_t L[KCAP];
-#pragma unroll
-  for (int j = 0; j < KCAP; ++j) L[j] = 0;
-  if (tid < kTileQ) {
-    const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
-    thr_score[tid] = seed;
-    thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
-  }
-  if (tid < 2) flag[tid] = 0;
-
-  // glds map: wave w fills rows [32w, 32w+32) of both tiles, 8 rows (1 KiB) per instruction;
-  // lane l lands at LDS slot (row 8j + l/8, physical chunk l%8) and so loads logical chunk
-  // (l%8) ^ swz(row) from global: the XOR swizzle moves to the source address.
-  const int ld_row = lane >> 3;
-  auto issue = [&](int s) {
-    const int t = t_begin + s / n_ktiles;
-    const int kt = s - (s / n_ktiles) * n_ktiles;
-    unsigned char* buf = smem + (s % ring::kStages) * ring::kStageBytes;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = wave * 32 + 8 * j + ld_row;
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      const int64_t goff = (int64_t)row * row_stride + kt * kRowBytes + c * 16;
-      glds16(corpus + (int64_t)t * kTileRows * row_stride + goff, buf + (wave * 32 + 8 * j) * kRowBytes);
-      glds16(queries + (int64_t)q0 * row_stride + goff,
-             buf + kTileRows * kRowBytes + (wave * 32 + 8 * j) * kRowBytes);
-    }
-  };
-  if (total > 0) issue(0);
-  if (total > 1) issue(1);
-  __syncthreads();  // thresholds visible (nothing in flight can be drained harmfully here? the two
-                    // prologue stages are: this costs one wait at start only)
-
-  f32x16 acc[2][2];
-  int round_id = 0;
-  for (int s = 0; s < total; ++s) {
-    if (s + 1 < total) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage s landed; s+1 may still fly
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    lds_barrier();  // every wave's stage-s data visible; every wave done with stage s-1
-    if (s + 2 < total) issue(s + 2);  // refills the buffer stage s-1 used
-    const int tk = s / n_ktiles;
-    const int kt = s - tk * n_ktiles;
-    if (kt == 0) {
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
-    }
-    const unsigned char* buf = smem + (s % ring::kStages) * ring::kStageBytes;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int ch = 2 * g + fh;
-      u32x4 a[2], b[2];
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-        a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-        b[bj] = *reinterpret_cast<const u32x4*>(buf + kTileRows * kRowBytes + swz(wq * 64 + bj * 32 + fr, ch));
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
-    }
-    if (kt != n_ktiles - 1) continue;
-
-    // ---- epilogue of corpus tile (t_begin + tk); the next tile's first stages are in flight
-    const int64_t r0 = (int64_t)(t_begin + tk) * kTileRows;
-    if (flags & kFlagSkipEpilogue) {
-      float sink = 0.f;
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
-      if (sink == 1234.5678f) part_keys[0] = 1;
-      continue;
-    }
-    uint64_t consumed = 0;
-    const int pid = wr * 2 + fh;
-    for (;;) {
-      ++round_id;
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj) {
-        const int ql = wq * 64 + bj * 32 + fr;
-        const float ths = (q0 + ql < n_q) ? thr_score[ql] : INFINITY;
-        const uint64_t thk = thr_key[ql];
-        float m = acc[0][bj][0];
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[bi][bj][r]);
-        int c = 0;
-        uint64_t flagged = __ballot(m >= ths);
-        if (flagged) {
-          if (m >= ths) {
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-              for (int c4 = 0; c4 < 4; ++c4) {
-                f32x4 v4 = {acc[bi][bj][4 * c4], acc[bi][bj][4 * c4 + 1], acc[bi][bj][4 * c4 + 2],
-                            acc[bi][bj][4 * c4 + 3]};
-                *reinterpret_cast<f32x4*>(scr + lane * 32 + bi * 16 + 4 * c4) = v4;
-              }
-          }
-          __builtin_amdgcn_wave_barrier();
-          const uint32_t cons_bj = (uint32_t)(consumed >> (bj * 32));
-          const uint32_t thk_lo = (uint32_t)thk, thk_hi = (uint32_t)(thk >> 32);
-          const int v = lane & 31;
-          const int row_v = (v >> 4) * 32 + (v & 3) + 8 * ((v >> 2) & 3);
-          while (flagged) {
-            const int fA = __builtin_ctzll(flagged);
-            flagged &= flagged - 1;
-            const int fB = flagged ? __builtin_ctzll(flagged) : fA;
-            const bool hasB = flagged != 0;
-            if (hasB) flagged &= flagged - 1;
-            const bool upper = lane >= 32;
-            const bool active = !upper || hasB;
-            const int f = upper ? fB : fA;
-            const float tsA = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fA));
-            const float tsB = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fB));
-            const uint64_t tkA = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fA) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fA);
-            const uint64_t tkB = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fB) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fB);
-            const uint32_t csA = (uint32_t)__builtin_amdgcn_readlane((int)cons_bj, fA);
-            const uint32_t csB = (uint32_t)__builtin_amdgcn_readlane((int)cons_bj, fB);
-            const int cA = __builtin_amdgcn_readlane(c, fA);
-            const int cB = __builtin_amdgcn_readlane(c, fB);
-            const float ts = upper ? tsB : tsA;
-            const uint64_t tk = upper ? tkB : tkA;
-            const uint32_t cs = upper ? csB : csA;
-            const int cf = upper ? cB : cA;
-            const float val = scr[f * 32 + v];
-            const int row = (int)r0 + wr * 64 + 4 * (f >> 5) + row_v;
-            bool pass = active && val >= ts && !((cs >> v) & 1u) && row < n_rows;
-            uint64_t key = 0;
-            if (pass) {
-              key = make_key(val, row_base + (uint32_t)row);
-              pass = key > tk;
-            }
-            const uint64_t bal = __ballot(pass);
-            const uint32_t half = upper ? (uint32_t)(bal >> 32) : (uint32_t)bal;
-            const int rank = __builtin_popcount(half & ((1u << v) - 1u));
-            const bool store = pass && cf + rank < ring::kProdCap;
-            if (store) {
-              const int qf = wq * 64 + bj * 32 + (f & 31);
-              const int pf = wr * 2 + (f >> 5);
-              cand[(qf * 4 + pf) * ring::kProdCap + cf + rank] = key;
-            }
-            const uint64_t sbal = __ballot(store);
-            const int totA = __builtin_popcount((uint32_t)bal);
-            const int totB = __builtin_popcount((uint32_t)(bal >> 32));
-            if (cA + totA > ring::kProdCap || (hasB && cB + totB > ring::kProdCap)) flag[round_id & 1] = round_id;
-            if (lane == fA) {
-              c = min(cA + totA, ring::kProdCap);
-              consumed |= (uint64_t)(uint32_t)sbal << (bj * 32);
-            }
-            if (hasB && lane == fB) {
-              c = min(cB + totB, ring::kProdCap);
-              consumed |= (uint64_t)(uint32_t)(sbal >> 32) << (bj * 32);
-            }
-          }
-        }
-        cnt[ql * 4 + pid] = c;
-      }
-      lds_barrier();
-      if (tid < kTileQ) {
-        bool changed = false;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int n = cnt[tid * 4 + u];
-          const uint64_t* src = cand + (tid * 4 + u) * ring::kProdCap;
-          for (int i = 0; i < n; ++i) list_insert<KCAP>(L, src[i]);
-          changed |= n > 0;
-        }
-        if (changed) {
-          const uint64_t kth = list_at<KCAP>(L, k_out - 1);
-          if (kth > thr_key[tid]) {
-            thr_key[tid] = kth;
-            thr_score[tid] = key_score(kth);
-          }
-        }
-      }
-      lds_barrier();
-      if (flag[round_id & 1] != round_id) break;
-    }
-  }
-
-  if (tid < kTileQ && q0 + tid < n_q) {
-    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
-#pragma unroll
-    for (int j = 0; j < KCAP; ++j)
-      if (j < k_out) dst[j] = L[j];
-  }
-}
-
-// =============================================================================================
-// wide: 256-row x 256-query workgroup tile (8 waves of 64 rows x 128 queries), one workgroup per
-// CU. A 128x128 tile needs 32 KiB of operands per 64-deep K-step for 2 MFLOP (64 FLOP/B): at
-// ~950 TFLOP/s that is ~58 GB/s per CU from L2, the per-CU L2 delivery the guide measures
-// (66-73 GB/s), so the tile shape, not MFMA issue, capped v1. 256x256 is 128 FLOP/B.
-// Operands stream through a 3-stage global_load_lds ring of 32-deep K-steps (64 B per row), kept
-// in flight across corpus tiles and across the epilogue (the epilogue's LDS is separate). The
-// epilogue screens flagged producer lanes two at a time through a 256-B per-wave scratch and
-// reserves slots of a per-query candidate buffer with one LDS atomic per flagged lane.
-// =============================================================================================
-namespace wide {
-constexpr int kThreads = 512;
-constexpr int kTileRows = 256;
-constexpr int kTileQ = 256;
+namespace lanek {
 constexpr int kRowBytes = 64;  // one k-tile of one row: 4 chunks of 16 B
-constexpr int kStageBytes = (kTileRows + kTileQ) * kRowBytes;  // 32 KiB
 
-// LDS map for a ring of STAGES slots (STAGES - 1 k-tiles in flight). The candidate buffer
-// shrinks as the ring grows so both fit in 160 KiB.
-template <int STAGES>
-struct Layout {
-  static constexpr int kSlots = STAGES >= 4 ? 8 : 16;            // candidates per query per round
-  static constexpr int kOffCand = STAGES * kStageBytes;
-  static constexpr int kCandBytes = kTileQ * kSlots * 8;
-  static constexpr int kOffScratch = kOffCand + kCandBytes;
-  static constexpr int kScratchBytes = 8 * 64 * 4;               // per wave: 2 lanes x 32 scores
-  static constexpr int kOffThrKey = kOffScratch + kScratchBytes;
-  static constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
-  static constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
-  static constexpr int kOffFlag = kOffCnt + kTileQ * 4;
-  static constexpr int kLdsBytes = kOffFlag + 16;
-  static_assert(kLdsBytes <= 160 * 1024, "wide kernel LDS exceeds 160 KiB");
-  static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
+template <int NB, int WAVES, int STAGES>
+struct Cfg {
+  static constexpr int kThreads = WAVES * 64;
+  static constexpr int kTileRows = 32 * NB;
+  static constexpr int kTileQ = 32 * WAVES;
+  static constexpr int kStageBytes = (kTileRows + kTileQ) * kRowBytes;
+  static constexpr int kLoadsPerWave = (kTileRows + kTileQ) / 16 / WAVES;  // 1-KiB DMA instructions
+  static constexpr int kLdsBytes = STAGES * kStageBytes;          // operand ring
+  static constexpr int kLdsTotal = kLdsBytes + kThreads * 64;     // + one 16-score slot per lane
+  static_assert((kTileRows + kTileQ) % (16 * WAVES) == 0, "tile rows must split evenly over waves");
+  static_assert(kTileRows % (16 * WAVES) == 0, "corpus rows must split evenly over waves");
+  static_assert(kLdsTotal <= 160 * 1024, "lane kernel LDS exceeds 160 KiB");
+  static_assert(WAVES * 64 * 16 * 8 <= kLdsTotal, "final list exchange (KCAP <= 16) must fit");
 };
 
 // 64-B rows: a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the row so the 16
@@ -765,27 +510,24 @@ struct Layout {
 __device__ __forceinline__ int swz(int row, int chunk) {
   return row * kRowBytes + ((chunk ^ ((row >> 2) & 3)) << 4);
 }
-}  // namespace wide
+}  // namespace lanek
 
-template <int DT, int KCAP, int STAGES>
-__global__ __launch_bounds__(wide::kThreads, 1) void topk_wide_kernel(
+template <int DT, int KCAP, int NB, int WAVES, int STAGES, int MINB>
+__global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
     int n_rows, int n_q, int n_ktiles, int n_splits, int n_row_tiles, uint32_t row_base, int k_out,
     uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int qblocks, int flags) {
-  using LY = wide::Layout<STAGES>;
-  using wide::kRowBytes;
-  using wide::kStageBytes;
-  using wide::swz;
-  constexpr int kSlots = LY::kSlots;
-  constexpr int kStages = STAGES;
-  constexpr int TR = wide::kTileRows;
-  constexpr int TQ = wide::kTileQ;
+  using C = lanek::Cfg<NB, WAVES, STAGES>;
+  using lanek::kRowBytes;
+  using lanek::swz;
+  constexpr int TR = C::kTileRows;
+  constexpr int TQ = C::kTileQ;
+  constexpr int LPW = C::kLoadsPerWave;
+  constexpr int LPW_C = TR / 16 / WAVES;  // of which corpus rows
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave & 3;   // 64-row quarter of the tile
-  const int wq = wave >> 2;  // 128-query half of the block
   const int fr = lane & 31;
   const int fh = lane >> 5;
   int split, qb;
@@ -799,240 +541,214 @@ __global__ __launch_bounds__(wide::kThreads, 1) void topk_wide_kernel(
     qb = blockIdx.x / n_splits;
   }
   const int q0 = qb * TQ;
-  // Contiguous, balanced tile ranges (sizes differ by at most one tile).
   const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
   const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
   const int total = (t_end - t_begin) * n_ktiles;
 
-  uint64_t* thr_key = reinterpret_cast<uint64_t*>(smem + LY::kOffThrKey);
-  float* thr_score = reinterpret_cast<float*>(smem + LY::kOffThrScore);
-  int* cnt = reinterpret_cast<int*>(smem + LY::kOffCnt);
-  int* flag = reinterpret_cast<int*>(smem + LY::kOffFlag);
-  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + LY::kOffCand);
-  float* scr = reinterpret_cast<float*>(smem + LY::kOffScratch) + wave * 64;
-
+  // this lane's query and its threshold: seed from the pre-pass, then the list's k-th key
+  const int q = q0 + wave * 32 + fr;
+  const bool q_ok = q < n_q;
+  float thr = q_ok ? ((thr_init) ? thr_init[q] : -INFINITY) : INFINITY;
+  uint64_t thk = (q_ok && thr != -INFINITY) ? (((uint64_t)ord_f32(thr) << 32) - 1) : 0;
+  const uint64_t thk_seed = thk;
   uint64_t L[KCAP];
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) L[j] = 0;
-  if (tid < TQ) {
-    const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
-    thr_score[tid] = seed;
-    thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
-    cnt[tid] = 0;
-  }
-  if (tid < 2) flag[tid] = 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init read retired before the ring counts
 
-  // glds map: wave w fills rows [32w, 32w+32) of the corpus tile and of the query tile, 16 rows
-  // (1 KiB) per instruction; lane l lands at (row 16j + l/4, physical chunk l%4) and loads the
-  // logical chunk (l%4) ^ swz(row) from global memory.
+  // ---- operand ring: wave w moves LPW_C 1-KiB pieces of the corpus tile and LPW - LPW_C of the
+  // query tile; lane l of a piece lands at (row 16p + l/4, physical chunk l%4).
   const int ld_row = lane >> 2;
-  const uint32_t tile_bytes = (uint32_t)(TR * row_stride);
-  const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, tile_bytes);
-  uint32_t ld_off[2];  // this lane's byte offset inside a tile, k-tile 0
+  const uint32_t c_bytes = (uint32_t)(TR * row_stride);
+  const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, (uint32_t)(TQ * row_stride));
+  uint32_t ld_off[LPW];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = wave * 32 + 16 * j + ld_row;
+  for (int j = 0; j < LPW; ++j) {
+    const int piece = wave * LPW + j;  // 0 .. (TR+TQ)/16 - 1 over the workgroup
+    const int prow = (piece < TR / 16) ? piece * 16 : (piece - TR / 16) * 16;
+    const int row = prow + ld_row;
     ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 3) ^ ((row >> 2) & 3)) << 4);
   }
   auto issue = [&](int s) {
     const int t = t_begin + s / n_ktiles;
     const int kt = s - (s / n_ktiles) * n_ktiles;
-    unsigned char* buf = smem + (s % kStages) * kStageBytes;
-    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)t * TR * row_stride, tile_bytes);
+    unsigned char* buf = smem + (s % STAGES) * C::kStageBytes;
+    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)t * TR * row_stride, c_bytes);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint32_t off = ld_off[j] + kt * kRowBytes;
-      blds16(c_rsrc, off, buf + (wave * 32 + 16 * j) * kRowBytes);
-      blds16(q_rsrc, off, buf + TR * kRowBytes + (wave * 32 + 16 * j) * kRowBytes);
+    for (int j = 0; j < LPW; ++j) {
+      const int piece = wave * LPW + j;
+      // corpus pieces first (rows 0..TR-1), then query pieces (LDS rows TR..TR+TQ-1)
+      blds16(piece < TR / 16 ? c_rsrc : q_rsrc, ld_off[j] + kt * kRowBytes, buf + piece * 16 * kRowBytes);
     }
   };
 #pragma unroll
   for (int i = 0; i < STAGES - 1; ++i)
     if (i < total) issue(i);
 
-  f32x16 acc[2][4];
-  int round_id = 0;
+  f32x16 acc[NB];
+  const int row_l = 4 * fh;  // + bi*32 + (r&3) + 8*(r>>2)
+  // per-lane 64-B slot after the operand ring: a passing 16-row group is staged here so the
+  // scan reads its scores with lane-varying LDS addresses instead of register select chains
+  float* slot = reinterpret_cast<float*>(smem + C::kLdsBytes) + (wave * 64 + lane) * 16;
+
+  const bool skip_epilogue = (flags & kFlagSkipEpilogue) != 0;
   for (int s = 0; s < total; ++s) {
-    // stage s landed: the 4 loads per later stage already issued (up to STAGES - 2) may fly
+    // stage s landed; the LPW loads of each later stage already issued may still fly
     if constexpr (STAGES >= 4) {
       if (s + 2 < total) {
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPW) : "memory");
       } else if (s + 1 < total) {
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else if constexpr (STAGES == 3) {
+      if (s + 1 < total) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPW) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     } else {
-      if (s + 1 < total) {
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();  // every wave's stage-s data visible; every wave done reading stage s-1
-    if (s + STAGES - 1 < total) issue(s + STAGES - 1);  // refills the slot stage s-1 used
+    if (s + STAGES - 1 < total) issue(s + STAGES - 1);
     const int tk = s / n_ktiles;
     const int kt = s - tk * n_ktiles;
     if (kt == 0) {
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[bi][r] = 0.f;
     }
-    const unsigned char* buf = smem + (s % kStages) * kStageBytes;
-    u32x4 fa0[2], fb0[4], fa1[2], fb1[4];
-    auto frag_load = [&](int g, u32x4 (&a)[2], u32x4 (&b)[4]) {
+    const unsigned char* buf = smem + (s % STAGES) * C::kStageBytes;
+    // Fragment schedule: the NB + 1 reads of k16 step 0, then step 0's MFMAs each paired with
+    // one read of step 1, then step 1's MFMAs. Reads stay ahead of their MFMAs (counted
+    // lgkmcnt waits, at most 15 outstanding: the counter's width) instead of the compiler's
+    // register-saving order, where every MFMA waits out an LDS latency.
+    u32x4 fb[2], fa[2][NB];
+    auto frag_reads = [&](int g) __attribute__((always_inline)) {
       const int ch = 2 * g + fh;
+      fb[g] = *reinterpret_cast<const u32x4*>(buf + TR * kRowBytes + swz(wave * 32 + fr, ch));
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-        a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
-#pragma unroll
-      for (int bj = 0; bj < 4; ++bj)
-        b[bj] = *reinterpret_cast<const u32x4*>(buf + TR * kRowBytes + swz(wq * 128 + bj * 32 + fr, ch));
+      for (int bi = 0; bi < NB; ++bi) fa[g][bi] = *reinterpret_cast<const u32x4*>(buf + swz(bi * 32 + fr, ch));
     };
-    auto frag_mma = [&](const u32x4 (&a)[2], const u32x4 (&b)[4]) {
+    frag_reads(0);
+    __builtin_amdgcn_sched_barrier(0);
+    frag_reads(1);
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+    for (int bi = 0; bi < NB; ++bi) mfma_step<DT>(fa[0][bi], fb[0], acc[bi]);
+    if constexpr (DT != DT_F32) {  // f32 steps are 4 MFMAs each: leave those to the scheduler
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
-    };
-    frag_load(0, fa0, fb0);
-    frag_load(1, fa1, fb1);
+      for (int i = 0; i < NB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
-    frag_mma(fa0, fb0);
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi) mfma_step<DT>(fa[1][bi], fb[1], acc[bi]);
     __builtin_amdgcn_sched_barrier(0);
-    frag_mma(fa1, fb1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt != n_ktiles - 1) continue;
+    if (kt != n_ktiles - 1 || skip_epilogue) continue;
 
-    // ---- epilogue of corpus tile (t_begin + tk); the next tile's first stages are in flight.
-    const int64_t r0 = (int64_t)(t_begin + tk) * TR;
-    if (flags & kFlagSkipEpilogue) {
-      float sink = 0.f;
+    // ---- lane-local epilogue of corpus tile t_begin + tk
+    const int r0 = (t_begin + tk) * TR;
+    uint32_t gmask = 0;  // 16-row groups whose max reaches the threshold
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+    for (int bi = 0; bi < NB; ++bi) {
+      float m0 = acc[bi][0], m1 = acc[bi][1];
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
-      if (sink == 1234.5678f) part_keys[0] = 1;
+      for (int r = 2; r < 16; r += 2) {
+        m0 = fmaxf(m0, acc[bi][r]);
+        m1 = fmaxf(m1, acc[bi][r + 1]);
+      }
+      gmask |= (fmaxf(m0, m1) >= thr ? 1u : 0u) << bi;
+    }
+    if (flags & kFlagMaxOnly) {
+      if (gmask == 0xFFFFFFFFu) part_keys[0] = 1;  // keep the maxima live
       continue;
     }
-    // Each query's 256 tile scores sit in 8 producer lanes (4 row-waves x 2 lane halves), 32
-    // registers each. consumed[bj] bit v: score v of column bj already handed over this tile.
-    uint32_t consumed[4] = {0u, 0u, 0u, 0u};
-    const int v = lane & 31;
-    const int row_v = (v >> 4) * 32 + (v & 3) + 8 * ((v >> 2) & 3);
-    const bool upper = lane >= 32;
-    for (;;) {
-      ++round_id;
+    // One passing group per lane per round: stage it (a static branch per group, taken only
+    // where some lane selected it), build its pass mask, then one list_insert per passing score
+    // in a divergent loop: the wave pays max-survivors-per-lane inserts.
+    while (__ballot(gmask != 0)) {
+      const int sel = gmask ? __builtin_ctz(gmask) : -1;
+      gmask &= gmask - 1;
 #pragma unroll
-      for (int bj = 0; bj < 4; ++bj) {
-        const int ql = wq * 128 + bj * 32 + fr;
-        const float ths = (q0 + ql < n_q) ? thr_score[ql] : INFINITY;
-        const uint64_t thk = thr_key[ql];
-        float m0 = acc[0][bj][0], m1 = acc[0][bj][1], m2 = acc[1][bj][0], m3 = acc[1][bj][1];
+      for (int bi = 0; bi < NB; ++bi) {
+        if (sel == bi) {
 #pragma unroll
-        for (int r = 2; r < 16; r += 2) {
-          m0 = fmaxf(m0, acc[0][bj][r]);
-          m1 = fmaxf(m1, acc[0][bj][r + 1]);
-          m2 = fmaxf(m2, acc[1][bj][r]);
-          m3 = fmaxf(m3, acc[1][bj][r + 1]);
-        }
-        const float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
-        uint64_t flagged = __ballot(m >= ths);
-        if (!flagged) continue;
-        const uint32_t thk_lo = (uint32_t)thk, thk_hi = (uint32_t)(thk >> 32);
-        while (flagged) {
-          const int fA = __builtin_ctzll(flagged);
-          flagged &= flagged - 1;
-          const bool hasB = flagged != 0;
-          const int fB = hasB ? __builtin_ctzll(flagged) : fA;
-          if (hasB) flagged &= flagged - 1;
-          // the two flagged lanes publish their 32 scores: A -> scr[0..31], B -> scr[32..63]
-          if (lane == fA || (hasB && lane == fB)) {
-            float* dst = scr + (lane == fA ? 0 : 32);
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-              for (int c4 = 0; c4 < 4; ++c4) {
-                f32x4 v4 = {acc[bi][bj][4 * c4], acc[bi][bj][4 * c4 + 1], acc[bi][bj][4 * c4 + 2],
-                            acc[bi][bj][4 * c4 + 3]};
-                *reinterpret_cast<f32x4*>(dst + bi * 16 + 4 * c4) = v4;
-              }
+          for (int c4 = 0; c4 < 4; ++c4) {
+            f32x4 v4 = {acc[bi][4 * c4], acc[bi][4 * c4 + 1], acc[bi][4 * c4 + 2], acc[bi][4 * c4 + 3]};
+            *reinterpret_cast<f32x4*>(slot + 4 * c4) = v4;
           }
-          __builtin_amdgcn_wave_barrier();
-          const int f = upper ? fB : fA;
-          // readlane needs a wave-uniform lane: read both flagged lanes' state, then select
-          const float tsA = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fA));
-          const float tsB = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ths), fB));
-          const float ts = upper ? tsB : tsA;
-          const uint64_t tk64 = upper
-              ? (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fB) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fB))
-              : (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thk_hi, fA) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)thk_lo, fA));
-          const uint32_t csA = (uint32_t)__builtin_amdgcn_readlane((int)consumed[bj], fA);
-          const uint32_t csB = (uint32_t)__builtin_amdgcn_readlane((int)consumed[bj], fB);
-          const uint32_t cs = upper ? csB : csA;
-          const float val = scr[lane];
-          const int row = (int)r0 + wr * 64 + 4 * (f >> 5) + row_v;
-          bool pass = (!upper || hasB) && val >= ts && !((cs >> v) & 1u) && row < n_rows;
-          uint64_t key = 0;
-          if (pass) {
-            key = make_key(val, row_base + (uint32_t)row);
-            pass = key > tk64;
-          }
-          const uint64_t bal = __ballot(pass);
-          const int totA = __builtin_popcount((uint32_t)bal);
-          const int totB = __builtin_popcount((uint32_t)(bal >> 32));
-          const int qA = wq * 128 + bj * 32 + (fA & 31);
-          const int qB = wq * 128 + bj * 32 + (fB & 31);
-          // slot reservation: one LDS atomic per flagged lane (lanes 0 and 32)
-          int got = 0;
-          if (v == 0) {
-            const int tot = upper ? totB : totA;
-            if (tot) got = atomicAdd(&cnt[upper ? qB : qA], tot);
-          }
-          const int baseA = __builtin_amdgcn_readlane(got, 0);
-          const int baseB = __builtin_amdgcn_readlane(got, 32);
-          const uint32_t half = upper ? (uint32_t)(bal >> 32) : (uint32_t)bal;
-          const int rank = __builtin_popcount(half & ((1u << v) - 1u));
-          const int base = upper ? baseB : baseA;
-          const bool store = pass && base + rank < kSlots;
-          if (store) cand[(upper ? qB : qA) * kSlots + base + rank] = key;
-          const uint64_t sbal = __ballot(store);
-          if (baseA + totA > kSlots || (hasB && baseB + totB > kSlots)) flag[round_id & 1] = round_id;
-          if (lane == fA) consumed[bj] |= (uint32_t)sbal;
-          if (hasB && lane == fB) consumed[bj] |= (uint32_t)(sbal >> 32);
         }
       }
-      lds_barrier();
-      if (tid < TQ) {
-        const int n = min(cnt[tid], kSlots);
-        if (n > 0) {
-          for (int i = 0; i < n; ++i) list_insert<KCAP>(L, cand[tid * kSlots + i]);
+      if (sel >= 0) {
+        const int rb = r0 + sel * 32 + row_l;
+        uint32_t pm = 0;
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * c4 + e;
+            pm |= (v4[e] >= thr && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
+          }
+        }
+        bool ins = false;
+        while (pm) {
+          const int r = __builtin_ctz(pm);
+          pm &= pm - 1;
+          const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
+          if (key > thk) {
+            list_insert<KCAP>(L, key);
+            ins = true;
+          }
+        }
+        if (ins) {
           const uint64_t kth = list_at<KCAP>(L, k_out - 1);
-          if (kth > thr_key[tid]) {
-            thr_key[tid] = kth;
-            thr_score[tid] = key_score(kth);
+          if (kth > thk) {
+            thk = kth;
+            thr = key_score(kth);
           }
-          cnt[tid] = 0;
         }
       }
-      lds_barrier();
-      // parity slots: a round-R overflow write never races a slower wave's read of round R-1
-      if (flag[round_id & 1] != round_id) break;
     }
   }
 
-  if (tid < TQ && q0 + tid < n_q) {
-    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+  if (skip_epilogue) {
+    float sink = 0.f;
 #pragma unroll
-    for (int j = 0; j < KCAP; ++j)
-      if (j < k_out) dst[j] = L[j];
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sink += acc[bi][r];
+    if (sink == 1234.5678f) part_keys[0] = 1;
+    return;
   }
+
+  // ---- merge the two half-wave lists of each query (lanes l, l+32) through LDS, then write
+  __syncthreads();  // every wave is done with the operand ring (all DMA retired at the last step)
+  uint64_t* xl = reinterpret_cast<uint64_t*>(smem) + (wave * 64 + lane) * KCAP;
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) xl[j] = L[j];
+  __builtin_amdgcn_wave_barrier();
+  if (fh == 0) {
+    const uint64_t* pl = xl + 32 * KCAP;  // partner lane l + 32
+    for (int j = 0; j < KCAP; ++j) {
+      const uint64_t kk = pl[j];
+      if (kk == 0 || kk <= L[KCAP - 1]) break;  // sorted: nothing further can enter
+      list_insert<KCAP>(L, kk);
+    }
+    if (q_ok) {
+      uint64_t* dst = part_keys + ((int64_t)q * n_splits + split) * k_out;
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j)
+        if (j < k_out) dst[j] = L[j];
+    }
+  }
+  (void)thk_seed;
 }
 
 // Merge n_lists sorted key lists per query into the top k. One wave per query: every lane
@@ -1317,7 +1033,8 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
     (void)hipEventRecord(ix->prof_events[(size_t)ix->prof_calls * (kStages + 1) + stage], s);
 }
 
-enum { KERNEL_V1 = 0, KERNEL_RING = 1, KERNEL_WIDE = 2 };
+// ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128
+enum { KERNEL_V1 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2 };
 
 struct SearchPlan {
   int kernel;
@@ -1330,32 +1047,31 @@ constexpr int64_t kRowPad = 256;
 // Below this batch the 256-query tile wastes MFMA work on padding; v1's 128 is used instead.
 constexpr int kWideMinBatch = 512;
 
-// Resident workgroups: v1 tile kernel 2 per CU (VGPR/LDS limited), ring kernel 1 per CU.
+// Resident workgroups of the 128x128 tile kernel: 2 per CU (VGPR/LDS limited).
 constexpr int kResidentSlotsV1 = 256 * 2;
-constexpr int kResidentSlotsRing = 256;
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
-  if (ix->debug_flags & kFlagUseRing) {
-    p.kernel = KERNEL_RING;
-  } else if (kcap_for(k) <= 16 && B >= kWideMinBatch && !(ix->debug_flags & kFlagNoWide)) {
-    p.kernel = KERNEL_WIDE;
-  } else {
-    p.kernel = KERNEL_V1;
-  }
-  if (p.kernel == KERNEL_WIDE) {
-    // One workgroup per CU; splits a multiple of 8 (rounded down: a 257th workgroup would run
-    // as a second wave) so the XCD remap keeps a split's query blocks on one XCD.
-    p.qblocks = (int)cdiv(B, wide::kTileQ);
-    p.n_row_tiles = (int)cdiv(ix->count, wide::kTileRows);
-    int want = std::max(1, 256 / p.qblocks);
+  p.kernel = KERNEL_V1;
+  if (k <= 16 && B >= kWideMinBatch && !(ix->debug_flags & kFlagTile128))
+    p.kernel = (ix->debug_flags & kFlagLane256q128) ? KERNEL_LANE256Q128 : KERNEL_LANE256;
+  if (p.kernel != KERNEL_V1) {
+    // Row tile TR, query tile TQ, `per_cu` resident workgroups per CU. One wave of workgroups;
+    // splits a multiple of 8 (rounded down: an extra workgroup would run as a second wave) so
+    // the XCD remap keeps a split's query blocks on one XCD.
+    const int TR = 256;
+    const int TQ = p.kernel == KERNEL_LANE256Q128 ? 128 : 256;
+    const int per_cu = p.kernel == KERNEL_LANE256Q128 ? 2 : 1;
+    p.qblocks = (int)cdiv(B, TQ);
+    p.n_row_tiles = (int)cdiv(ix->count, TR);
+    int want = std::max(1, 256 * per_cu / p.qblocks);
     want = std::min(want, std::max(1, p.n_row_tiles));
     p.xcd_remap = want >= 8;
     p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     return p;
   }
-  const int kResidentSlots = p.kernel == KERNEL_RING ? kResidentSlotsRing : kResidentSlotsV1;
+  const int kResidentSlots = kResidentSlotsV1;
   p.qblocks = (int)cdiv(B, kTileQ);
   p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
   // One wave of workgroups that fills every resident slot; splits padded to a multiple of 8
@@ -1383,7 +1099,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
   const int64_t qblocks = cdiv(B, kTileQ);
   const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlotsV1, qblocks)), 8) * 8;
-  const int64_t wide_splits = std::max<int64_t>(1, 256 / cdiv(B, wide::kTileQ));  // >= plan's
+  const int64_t wide_splits = std::max<int64_t>(1, 512 / cdiv(B, 128));  // >= any plan's
   const int64_t p_need =
       (int64_t)B * std::max<int64_t>(std::max(max_splits, wide_splits), kSampleMax / kTileRows) * k;
   if (p_need > ix->part_cap) {
@@ -1423,35 +1139,28 @@ void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_s
                      n_splits, qblocks, flags);
 }
 
-template <int DT, int KCAP>
-void launch_ring(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+template <int DT, int KCAP, int NB, int WAVES, int STAGES, int MINB>
+void launch_lane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                  const float* thr, int flags, hipStream_t s) {
+  using C = lanek::Cfg<NB, WAVES, STAGES>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_ring_kernel<DT, KCAP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, ring::kLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_lane_kernel<DT, KCAP, NB, WAVES, STAGES, MINB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsTotal);
     attr_set = true;
   }
-  hipLaunchKernelGGL((topk_ring_kernel<DT, KCAP>), dim3((unsigned)(p.n_splits * p.qblocks)), dim3(kThreads),
-                     ring::kLdsBytes, s, ix->rows, ix->qbuf, ix->row_stride, n_rows, B,
-                     ix->d_pad * ix->elem / kRowBytes, p.tiles_per_split, p.n_row_tiles, row_base, k, ix->part,
-                     thr, p.n_splits, p.qblocks, flags);
+  hipLaunchKernelGGL((topk_lane_kernel<DT, KCAP, NB, WAVES, STAGES, MINB>), dim3((unsigned)(p.n_splits * p.qblocks)),
+                     dim3(C::kThreads), C::kLdsTotal, s, ix->rows, ix->qbuf, ix->row_stride, n_rows, B,
+                     ix->d_pad * ix->elem / lanek::kRowBytes, p.n_splits, p.n_row_tiles, row_base, k, ix->part, thr,
+                     p.qblocks, flags);
 }
 
-template <int DT, int KCAP, int STAGES>
-void launch_wide(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
-                 const float* thr, int flags, hipStream_t s) {
-  constexpr int lds = wide::Layout<STAGES>::kLdsBytes;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_wide_kernel<DT, KCAP, STAGES>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((topk_wide_kernel<DT, KCAP, STAGES>), dim3((unsigned)(p.n_splits * p.qblocks)),
-                     dim3(wide::kThreads), lds, s, ix->rows, ix->qbuf, ix->row_stride, n_rows, B,
-                     ix->d_pad * ix->elem / wide::kRowBytes, p.n_splits, p.n_row_tiles, row_base, k, ix->part,
-                     thr, p.qblocks, flags);
+template <int DT, int NB, int WAVES, int STAGES, int MINB>
+void launch_lane_k(int kc, const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                   const float* thr, int flags, hipStream_t s) {
+  if (kc == 8) launch_lane<DT, 8, NB, WAVES, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  else if (kc == 12) launch_lane<DT, 12, NB, WAVES, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  else launch_lane<DT, 16, NB, WAVES, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
 }
 
 template <int DT>
@@ -1473,23 +1182,13 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
-  if (p.kernel == KERNEL_WIDE) {
-    const bool deep = (flags & kFlagWideStages4) == 0;  // 4 stages by default; flag 16 = 3 stages
-    if (kcap_for(k) == 8) {
-      if (deep) launch_wide<DT, 8, 4>(ix, p, n, B, k, row_base, thr, flags, s);
-      else launch_wide<DT, 8, 3>(ix, p, n, B, k, row_base, thr, flags, s);
-    } else {
-      if (deep) launch_wide<DT, 16, 4>(ix, p, n, B, k, row_base, thr, flags, s);
-      else launch_wide<DT, 16, 3>(ix, p, n, B, k, row_base, thr, flags, s);
-    }
-    return;
-  }
-  if (p.kernel == KERNEL_RING) {
-    switch (kcap_for(k)) {
-      case 8: launch_ring<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s); break;
-      case 16: launch_ring<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s); break;
-      default: launch_ring<DT, 32>(ix, p, n, B, k, row_base, thr, flags, s); break;
-    }
+  if (p.kernel != KERNEL_V1) {
+    // lane lists sized to k: 8, 12 or 16 keys (insert and select cost scale with the size)
+    const int kc = k <= 8 ? 8 : (k <= 12 ? 12 : 16);
+    if (p.kernel == KERNEL_LANE256Q128)
+      launch_lane_k<DT, 8, 4, 2, 2>(kc, ix, p, n, B, k, row_base, thr, flags, s);
+    else
+      launch_lane_k<DT, 8, 8, 4, 1>(kc, ix, p, n, B, k, row_base, thr, flags, s);
     return;
   }
   switch (kcap_for(k)) {
@@ -1736,7 +1435,7 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagUseRing | kFlagNoWide | kFlagWideStages4);
+  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kKernelFlags);
   return AHR_OK;
 }
 

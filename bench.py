@@ -208,6 +208,7 @@ def main() -> None:
         elem = 4 if dtype == "f32" else 2
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
         plan = local.plan(B, k)
+        kname = "topk_lane_kernel" if plan["kernel"].startswith("lane") else "topk_tile_kernel"
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -231,13 +232,13 @@ def main() -> None:
             },
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
             "roofline": {
-                "kernel": "topk_tile_kernel (fused MFMA Q.N^T + top-k)",
+                "kernel": f"{kname} (fused MFMA Q.N^T + top-k, {plan['kernel']})",
                 "bound": "mfma",
                 "achieved": round(achieved_tf, 2),
                 "peak": peak,
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / peak, 4),
-                "traffic": read_traffic("topk_tile_kernel"),
+                "traffic": read_traffic(kname),
                 "algorithmic_flops_per_launch": flops,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "hbm_equiv_GBs": round(alg_bytes / (tile_ms * 1e-3) / 1e9, 1),

@@ -99,13 +99,14 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_c
 /* Rows scored by the threshold pre-pass (0 disables it; else a power of two in [128, 1024]). */
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
-/* Ablation switches for profiling: 2 = skip the top-k epilogue (GEMM cost only, results are
- * garbage); 4 = use the 128x128 glds-ring tile kernel; 8 = never use the 256x256 wide kernel;
- * 16 = wide kernel with a 3-stage ring (4, 8 and 16 give correct results). Never set in production. */
+/* Ablation switches for profiling, never set in production: 2 = skip the top-k epilogue (GEMM
+ * cost only, results are garbage); 8 = always the 128x128 tile kernel; 64 = lane kernel with a
+ * 256x128 workgroup tile; 256 = lane kernel epilogue stops after the group maxima (garbage).
+ * 8 and 64 give correct results. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
- * *kernel: 0 = 128x128 tile kernel, 1 = 128x128 glds-ring kernel, 2 = 256x256 wide kernel. */
+ * *kernel: 0 = 128x128 tile kernel, 1 = 256x256 lane kernel, 2 = 256x128 lane kernel. */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 

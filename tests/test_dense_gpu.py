@@ -186,16 +186,16 @@ def test_many_lists_merge(cuda):
     np.testing.assert_array_equal(s, es.astype(np.float32))
 
 
-# ---- 256x256 wide kernel (B >= 512, k <= 16) --------------------------------------------------
+# ---- lane kernels (B >= 512, k <= 16): per-lane register top-k lists --------------------------
 
 @pytest.mark.parametrize("n,d,B,k", [(12000, 384, 700, 10), (3001, 256, 1500, 16), (5000, 768, 513, 5)])
-def test_wide_f32_bit_exact(cuda, n, d, B, k):
+def test_lane_f32_bit_exact(cuda, n, d, B, k):
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(2000 + n + B)
     C = _clustered(rng, n, d)
     Q = _clustered(rng, B, d)
     ix = DenseIndex(d, n, dtype="f32", device=cuda)
-    assert ix.plan(B, k)["kernel"] == "wide256"
+    assert ix.plan(B, k)["kernel"] == "lane256"
     ix.close()
     s, r = _run("f32", C, Q, k, cuda)
     es, er = dr.topk(C, Q, k, mode="fma")
@@ -204,7 +204,7 @@ def test_wide_f32_bit_exact(cuda, n, d, B, k):
 
 
 @pytest.mark.parametrize("k,sample", [(10, 8192), (16, 8192), (5, 0), (10, 0), (1, 8192)])
-def test_wide_equals_tile128(cuda, k, sample):
+def test_lane_equals_tile128(cuda, k, sample):
     """Both kernels chain the same 16-deep MFMA steps in k order: bitwise equal results. Sample 0
     (no pre-pass) starts every tile with 256 candidates per query: exercises overflow rounds."""
     from ah_rag.embeddings import DenseIndex
@@ -214,20 +214,19 @@ def test_wide_equals_tile128(cuda, k, sample):
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     ix.set_sample_rows(sample)
-    assert ix.plan(len(Q), k)["kernel"] == "wide256"
+    assert ix.plan(len(Q), k)["kernel"] == "lane256"
     a = [t.cpu().numpy() for t in ix.query(Q, k)]
-    ix.set_debug_flags(8)
-    assert ix.plan(len(Q), k)["kernel"] == "tile128"
-    b = [t.cpu().numpy() for t in ix.query(Q, k)]
-    ix.set_debug_flags(16)  # wide kernel with the 3-stage ring / 16-slot candidate buffer
-    c = [t.cpu().numpy() for t in ix.query(Q, k)]
+    # 8: 128x128 tile kernel; 64: lane kernel with 256x128 workgroup tiles
+    for flags, name in ((8, "tile128"), (64, "lane256x128")):
+        ix.set_debug_flags(flags)
+        assert ix.plan(len(Q), k)["kernel"] == name
+        b = [t.cpu().numpy() for t in ix.query(Q, k)]
+        np.testing.assert_array_equal(a[1], b[1], err_msg=name)
+        np.testing.assert_array_equal(a[0], b[0], err_msg=name)
     ix.close()
-    for x in (b, c):
-        np.testing.assert_array_equal(a[1], x[1])
-        np.testing.assert_array_equal(a[0], x[0])
 
 
-def test_wide_ties_order_by_row(cuda):
+def test_lane_ties_order_by_row(cuda):
     """Duplicate corpus rows tie exactly: lower row id first, across tiles and splits."""
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(12)

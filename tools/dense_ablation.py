@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="prod:8192:0,v1:8192:8,no_prepass:0:0,gemm_only:0:2,v1_gemm_only:0:10")
+    ap.add_argument("--variants", default="prod:8192:0,tile128:8192:8,lane256x128:8192:64,no_prepass:0:0,gemm_only:0:2,max_only:8192:256")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     spec = HOTPOT_90K if a.workload == "hotpot90k" else SYNTH_5M
