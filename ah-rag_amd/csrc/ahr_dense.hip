@@ -117,11 +117,6 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
 // LDS-DMA through a buffer descriptor (MUBUF `buffer_load ... lds`). Unlike the FLAT-encoded
 // global_load_lds, LLVM does not count it as a possibly out-of-order LDS access, so the
 // fragment reads that follow keep counted lgkmcnt(N) waits. The descriptor covers one tile
@@ -220,8 +215,10 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
     qb = blockIdx.x / n_splits;
   }
   const int q0 = qb * kTileQ;
-  const int t_begin = split * tiles_per_split;
-  const int t_end = min(t_begin + tiles_per_split, n_row_tiles);
+  // contiguous, balanced tile ranges (sizes differ by at most one tile)
+  const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
+  const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
+  (void)tiles_per_split;
 
   uint64_t* thr_key = reinterpret_cast<uint64_t*>(smem + kOffThrKey);
   float* thr_score = reinterpret_cast<float*>(smem + kOffThrScore);
@@ -247,17 +244,24 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
   const int ld_row = lane >> 3;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   int round_id = 0;
+  const uint32_t tile_bytes = (uint32_t)(kTileRows * row_stride);
+  const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, tile_bytes);
+  uint32_t ld_off[4];  // this lane's byte offset inside a tile, k-tile 0
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave_u * 32 + 8 * j + ld_row;
+    ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+  }
 
   for (int t = t_begin; t < t_end; ++t) {
     const int64_t r0 = (int64_t)t * kTileRows;
+    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + r0 * row_stride, tile_bytes);
     auto stage = [&](int kt, unsigned char* buf) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int row = wave_u * 32 + 8 * j + ld_row;
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
-        const int64_t goff = (int64_t)row * row_stride + kt * kRowBytes + c * 16;
-        glds16(corpus + r0 * row_stride + goff, buf + (wave_u * 32 + 8 * j) * kRowBytes);
-        glds16(queries + (int64_t)q0 * row_stride + goff, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
+        const uint32_t off = ld_off[j] + kt * kRowBytes;
+        blds16(c_rsrc, off, buf + (wave_u * 32 + 8 * j) * kRowBytes);
+        blds16(q_rsrc, off, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
       }
     };
     stage(0, smem + kOffBuf0);
@@ -651,7 +655,6 @@ __global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
     for (int bi = 0; bi < NB; ++bi) mfma_step<DT>(fa[1][bi], fb[1], acc[bi]);
     __builtin_amdgcn_sched_barrier(0);
     if (kt != n_ktiles - 1 || skip_epilogue) continue;
-
     // ---- lane-local epilogue of corpus tile t_begin + tk
     const int r0 = (t_begin + tk) * TR;
     uint32_t gmask = 0;  // 16-row groups whose max reaches the threshold
@@ -789,7 +792,7 @@ constexpr int kSampleMax = 16384;              // sampled rows
 constexpr int kGroupMax = kSampleMax / 16;        // group maxima per query
 
 // One wave per query: the k-th largest ordered value is found bit by bit from the MSB
-// (largest t with #{v >= t} >= k), 32 counting passes over 16 values per lane.
+// (largest t with #{v >= t} >= k), one counting pass per bit over <= 16 values per lane.
 __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict__ scores, int S,
                                                         int k, float* __restrict__ thr) {
   const int q = blockIdx.x;
@@ -801,8 +804,10 @@ __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict_
     const int i = lane + 64 * j;
     v[j] = i < S ? ord_f32(src[i]) : 0u;
   }
+  // 20 bits from the MSB (sign, exponent, 11 mantissa bits): ans is the largest 20-bit prefix
+  // with #{v >= ans} >= k, so ans <= the k-th largest value: a valid, ~5e-4-relative bound.
   uint32_t ans = 0;
-  for (int b = 31; b >= 0; --b) {
+  for (int b = 31; b >= 12; --b) {
     const uint32_t cand = ans | (1u << b);
     // count over the wave with ballots: scalar popcounts, no cross-lane data movement
     int c = 0;
@@ -1044,8 +1049,9 @@ struct SearchPlan {
 
 // Corpus and query buffers are padded to whole 256-row tiles (the wide kernel's tile).
 constexpr int64_t kRowPad = 256;
-// Below this batch the 256-query tile wastes MFMA work on padding; v1's 128 is used instead.
-constexpr int kWideMinBatch = 512;
+// The 256x256 lane kernel from this batch on; below it the 128x128 tile kernel is faster
+// (measured on MI355X, hotpot90k: equal-ish at 1024, lane 10-15 % ahead from 1536).
+constexpr int kWideMinBatch = 1025;
 
 // Resident workgroups of the 128x128 tile kernel: 2 per CU (VGPR/LDS limited).
 constexpr int kResidentSlotsV1 = 256 * 2;
@@ -1060,8 +1066,8 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     // splits a multiple of 8 (rounded down: an extra workgroup would run as a second wave) so
     // the XCD remap keeps a split's query blocks on one XCD.
     const int TR = 256;
-    const int TQ = p.kernel == KERNEL_LANE256Q128 ? 128 : 256;
-    const int per_cu = p.kernel == KERNEL_LANE256Q128 ? 2 : 1;
+    const int TQ = p.kernel == KERNEL_LANE256 ? 256 : 128;
+    const int per_cu = p.kernel == KERNEL_LANE256 ? 1 : 2;
     p.qblocks = (int)cdiv(B, TQ);
     p.n_row_tiles = (int)cdiv(ix->count, TR);
     int want = std::max(1, 256 * per_cu / p.qblocks);
@@ -1074,14 +1080,14 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   const int kResidentSlots = kResidentSlotsV1;
   p.qblocks = (int)cdiv(B, kTileQ);
   p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
-  // One wave of workgroups that fills every resident slot; splits padded to a multiple of 8
-  // so the XCD remap keeps a split's query blocks on one XCD.
-  int64_t want = std::max<int64_t>(1, cdiv(kResidentSlots, p.qblocks));
-  want = std::min<int64_t>(want, std::max(1, p.n_row_tiles));
-  p.tiles_per_split = std::max(1, (int)cdiv(p.n_row_tiles, want));
-  p.n_splits = std::max(1, (int)cdiv(p.n_row_tiles, p.tiles_per_split));
-  p.xcd_remap = p.n_splits >= 8;
-  if (p.xcd_remap) p.n_splits = (int)cdiv(p.n_splits, 8) * 8;
+  // One wave of workgroups: at most the resident slots, splits rounded DOWN to a multiple of 8
+  // (an extra workgroup would run as a second wave) so the XCD remap keeps a split's query
+  // blocks on one XCD; the kernel balances tile ranges over the splits.
+  int want = std::max(1, kResidentSlots / p.qblocks);
+  want = std::min(want, std::max(1, p.n_row_tiles));
+  p.xcd_remap = want >= 8;
+  p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+  p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
   return p;
 }
 

@@ -188,7 +188,7 @@ def test_many_lists_merge(cuda):
 
 # ---- lane kernels (B >= 512, k <= 16): per-lane register top-k lists --------------------------
 
-@pytest.mark.parametrize("n,d,B,k", [(12000, 384, 700, 10), (3001, 256, 1500, 16), (5000, 768, 513, 5)])
+@pytest.mark.parametrize("n,d,B,k", [(12000, 384, 1100, 10), (3001, 256, 1500, 16), (5000, 768, 1025, 5)])
 def test_lane_f32_bit_exact(cuda, n, d, B, k):
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(2000 + n + B)
