@@ -16,16 +16,17 @@
 // Kernels (both keep the score tile in MFMA accumulators, never in memory; corpus rows are the
 // A operand and queries the B operand of 32x32 MFMAs, so each lane's accumulator column is ONE
 // query and its registers are corpus rows of it):
-//  * topk_lane_kernel (default for B >= 512, k <= 16): a workgroup of 8 waves owns a 256-query
+//  * topk_lane_kernel (B >= 6144, k <= 16): a workgroup of 8 waves owns a 256-query
 //    block and a contiguous range of 256-row corpus tiles; each wave covers all 256 rows for its
 //    32 queries, so every lane keeps its query's partial top-k list in registers and screens its
 //    own scores (16-row group maxima against its threshold, scan of the rare passing groups):
 //    no candidate buffers, atomics or barriers in the epilogue. Operands stream through a
 //    4-stage buffer LDS-DMA ring. The two half-wave lists merge at the end.
-//  * topk_tile_kernel (small batches, k > 16, and the threshold pre-pass): 4 waves (2 along rows
-//    x 2 along queries), 128-query block x 128-row tiles, two workgroups per CU; survivors are
-//    screened cooperatively into per-query LDS candidate lists that one owner thread per query
-//    folds into its register top-k list.
+//  * topk_tile_kernel (default up to B < 6144, every k, and the threshold pre-pass): 4 waves
+//    (2 along rows x 2 along queries), 128-query block x 128-row tiles, two workgroups per CU.
+//    k <= 16: the same lane-local epilogue (each lane holds two query columns, so two lists;
+//    the 4 partial lists of a query merge at the end). k > 16: survivors are screened
+//    cooperatively into per-query LDS candidate lists that one owner thread per query folds.
 // The pre-pass (first 8192 rows, 16-row group maxima, k-th largest per query) seeds every
 // query's threshold with a valid lower bound of its final k-th best score.
 #include "ahr_common.h"
@@ -226,17 +227,34 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
   int* flag = reinterpret_cast<int*>(smem + kOffFlag);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + kOffCand);
 
+  // k <= 16: lane-local top-k (each lane keeps lists for its two query columns, screens its
+  // own scores; no LDS candidate buffers, no epilogue barriers). k > 16: cooperative screening
+  // into per-query LDS candidate lists folded by one owner thread per query.
+  constexpr bool LANE = MODE == MODE_TOPK && KCAP <= 16;
   uint64_t L[KCAP];
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) L[j] = 0;
-  if (tid < kTileQ) {
+  uint64_t LL[2][LANE ? KCAP : 1];
+  float lthr[2];
+  uint64_t lthk[2];
+  if constexpr (LANE) {
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) LL[bj][j] = 0;
+      const int q = q0 + wq * 64 + bj * 32 + fr;
+      lthr[bj] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+      lthk[bj] = (q < n_q && lthr[bj] != -INFINITY) ? (((uint64_t)ord_f32(lthr[bj]) << 32) - 1) : 0;
+    }
+  }
+  if (!LANE && tid < kTileQ) {
     // A row whose score equals the seed may still win on the row tie-break: the seed key is
     // the smallest key with that score, minus one.
     const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
     thr_score[tid] = seed;
     thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
   }
-  if (tid < 2) flag[tid] = 0;
+  if (!LANE && tid < 2) flag[tid] = 0;
 
   // Staging by global_load_lds (no staging registers): wave w fills rows [32w, 32w+32) of both
   // tiles, 8 rows (1 KiB) per instruction; lane l lands at (row 8j + l/8, physical chunk l%8) and
@@ -333,6 +351,83 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
       }
       __syncthreads();
       continue;
+    }
+
+    if constexpr (LANE) {
+      if (!(flags & kFlagSkipEpilogue)) {
+        // 16-row groups (bi, bj) whose max reaches the column's threshold; one group per lane
+        // per round is staged into the lane's 64-B slot in the second staging buffer (idle
+        // here: the next tile refills it only after the barrier behind its first stage, which
+        // every wave reaches after its epilogue) and scanned from there.
+        uint32_t gmask = 0;
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) {
+            float m0 = acc[bi][bj][0], m1 = acc[bi][bj][1];
+#pragma unroll
+            for (int r = 2; r < 16; r += 2) {
+              m0 = fmaxf(m0, acc[bi][bj][r]);
+              m1 = fmaxf(m1, acc[bi][bj][r + 1]);
+            }
+            gmask |= (fmaxf(m0, m1) >= lthr[bj] ? 1u : 0u) << (bj * 2 + bi);
+          }
+        float* slot = reinterpret_cast<float*>(smem + kOffBuf1) + tid * 16;
+        while (__ballot(gmask != 0)) {
+          const int sel = gmask ? __builtin_ctz(gmask) : -1;
+          gmask &= gmask - 1;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (sel == g) {
+#pragma unroll
+              for (int c4 = 0; c4 < 4; ++c4) {
+                f32x4 v4 = {acc[g & 1][g >> 1][4 * c4], acc[g & 1][g >> 1][4 * c4 + 1], acc[g & 1][g >> 1][4 * c4 + 2],
+                            acc[g & 1][g >> 1][4 * c4 + 3]};
+                *reinterpret_cast<f32x4*>(slot + 4 * c4) = v4;
+              }
+            }
+          }
+          if (sel >= 0) {
+            const int bjs = sel >> 1;
+            const int rb = (int)r0 + wr * 64 + (sel & 1) * 32 + 4 * fh;
+            const float th = bjs ? lthr[1] : lthr[0];
+            uint32_t pm = 0;
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+              const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int r = 4 * c4 + e;
+                pm |= (v4[e] >= th && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
+              }
+            }
+            while (pm) {
+              const int r = __builtin_ctz(pm);
+              pm &= pm - 1;
+              const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
+              if (bjs == 0) {
+                if (key > lthk[0]) list_insert<KCAP>(LL[0], key);
+              } else {
+                if (key > lthk[1]) list_insert<KCAP>(LL[1], key);
+              }
+            }
+            if (bjs == 0) {
+              const uint64_t kth = list_at<KCAP>(LL[0], k_out - 1);
+              if (kth > lthk[0]) {
+                lthk[0] = kth;
+                lthr[0] = key_score(kth);
+              }
+            } else {
+              const uint64_t kth = list_at<KCAP>(LL[1], k_out - 1);
+              if (kth > lthk[1]) {
+                lthk[1] = kth;
+                lthr[1] = key_score(kth);
+              }
+            }
+          }
+        }
+        continue;
+      }
     }
 
     if (flags & kFlagSkipEpilogue) {  // ablation: GEMM only, keep acc live, no top-k
@@ -471,7 +566,36 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
     }
   }
 
-  if (MODE == MODE_TOPK && tid < kTileQ && q0 + tid < n_q) {
+  if constexpr (LANE) {
+    // merge the 4 partial lists of each query (2 row-waves x 2 lane halves) through LDS
+    __syncthreads();  // staging buffers idle: every wave is past its last K-step
+    uint64_t* xl = reinterpret_cast<uint64_t*>(smem);
+    const int part = wr * 2 + fh;
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+      const int ql = wq * 64 + bj * 32 + fr;
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) xl[(ql * 4 + part) * KCAP + j] = LL[bj][j];
+    }
+    __syncthreads();
+    if (tid < kTileQ && q0 + tid < n_q) {
+      uint64_t M[KCAP];
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) M[j] = xl[(tid * 4) * KCAP + j];
+      for (int u = 1; u < 4; ++u) {
+        const uint64_t* src = xl + (tid * 4 + u) * KCAP;
+        for (int j = 0; j < KCAP; ++j) {
+          const uint64_t kk = src[j];
+          if (kk <= M[KCAP - 1]) break;  // sorted: nothing further can enter
+          list_insert<KCAP>(M, kk);
+        }
+      }
+      uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j)
+        if (j < k_out) dst[j] = M[j];
+    }
+  } else if (MODE == MODE_TOPK && tid < kTileQ && q0 + tid < n_q) {
     uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
 #pragma unroll
     for (int j = 0; j < KCAP; ++j)
@@ -1049,9 +1173,10 @@ struct SearchPlan {
 
 // Corpus and query buffers are padded to whole 256-row tiles (the wide kernel's tile).
 constexpr int64_t kRowPad = 256;
-// The 256x256 lane kernel from this batch on; below it the 128x128 tile kernel is faster
-// (measured on MI355X, hotpot90k: equal-ish at 1024, lane 10-15 % ahead from 1536).
-constexpr int kWideMinBatch = 1025;
+// The 256x256 lane kernel from this batch on; below it the 128x128 tile kernel (with its
+// lane-local epilogue) is as fast or faster (MI355X, hotpot90k: tile 128 ahead up to 2048,
+// even at 4096, lane 256 ~5 % ahead at 8192).
+constexpr int kWideMinBatch = 6144;
 
 // Resident workgroups of the 128x128 tile kernel: 2 per CU (VGPR/LDS limited).
 constexpr int kResidentSlotsV1 = 256 * 2;
@@ -1197,8 +1322,9 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       launch_lane_k<DT, 8, 8, 4, 1>(kc, ix, p, n, B, k, row_base, thr, flags, s);
     return;
   }
-  switch (kcap_for(k)) {
+  switch (k <= 8 ? 8 : (k <= 12 ? 12 : (k <= 16 ? 16 : 32))) {  // lists sized to k
     case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
+    case 12: launch_tile<DT, 12, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
     case 16: launch_tile<DT, 16, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
     default: launch_tile<DT, 32, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;
   }

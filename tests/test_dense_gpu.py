@@ -188,7 +188,7 @@ def test_many_lists_merge(cuda):
 
 # ---- lane kernels (B >= 512, k <= 16): per-lane register top-k lists --------------------------
 
-@pytest.mark.parametrize("n,d,B,k", [(12000, 384, 1100, 10), (3001, 256, 1500, 16), (5000, 768, 1025, 5)])
+@pytest.mark.parametrize("n,d,B,k", [(3000, 256, 6200, 10), (1001, 128, 6144, 16), (2000, 384, 6500, 5)])
 def test_lane_f32_bit_exact(cuda, n, d, B, k):
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(2000 + n + B)
@@ -205,12 +205,12 @@ def test_lane_f32_bit_exact(cuda, n, d, B, k):
 
 @pytest.mark.parametrize("k,sample", [(10, 8192), (16, 8192), (5, 0), (10, 0), (1, 8192)])
 def test_lane_equals_tile128(cuda, k, sample):
-    """Both kernels chain the same 16-deep MFMA steps in k order: bitwise equal results. Sample 0
-    (no pre-pass) starts every tile with 256 candidates per query: exercises overflow rounds."""
+    """All kernels chain the same 16-deep MFMA steps in k order: bitwise equal results. Sample 0
+    (no pre-pass) makes every score of the first tiles a candidate: full scans / overflow rounds."""
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(31 + k + sample)
-    C = _clustered(rng, 70001, 768)
-    Q = _clustered(rng, 1030, 768)
+    C = _clustered(rng, 40001, 768)   # >= 4 x 8192 rows: the pre-pass runs when sample > 0
+    Q = _clustered(rng, 6150, 768)    # >= 6144: the 256x256 lane kernel is the default
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     ix.set_sample_rows(sample)
