@@ -179,6 +179,7 @@ enum {
   kFlagTile128 = 8,       // always the 128x128 tile kernel
   kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
   kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
+  kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
 };
 constexpr int kKernelFlags = kFlagTile128 | kFlagLane256q128;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
@@ -282,7 +283,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
         blds16(q_rsrc, off, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
       }
     };
-    stage(0, smem + kOffBuf0);
+    const bool load = !(flags & kFlagNoLoads) || t == t_begin;  // ablation: LDS + MFMA ceiling
+    if (load) stage(0, smem + kOffBuf0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
 
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
         for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
 
     for (int kt = 0; kt < n_ktiles; ++kt) {
-      if (kt + 1 < n_ktiles) stage(kt + 1, smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0));
+      if (kt + 1 < n_ktiles && load) stage(kt + 1, smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0));
       const unsigned char* buf = smem + ((kt & 1) ? kOffBuf1 : kOffBuf0);
       // Two fragment register sets, order pinned with sched_barrier: the LDS reads of step g+1
       // are in flight while the MFMAs of step g run.
@@ -604,32 +606,36 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
 }
 
 // =============================================================================================
-// lane kernel: every wave covers ALL rows of the workgroup's corpus tile for its own 32 queries
-// (MFMA 32x32: the corpus rows are the A operand, NB row blocks; the wave's 32 queries are B),
-// so each lane's accumulator column is one query and the lane keeps that query's partial top-k
-// list in registers. The epilogue is then lane-local: per 16-row group a max and a compare with
-// the lane's threshold; only groups that reach it are scanned and inserted. No LDS candidate
-// buffers, atomics or barriers, so nothing in the epilogue waits on another wave, and with two
-// workgroups per CU one workgroup's epilogue runs beside the other's MFMAs. The two half-wave
-// lists of a query (lanes l and l+32 hold disjoint rows) are merged once, at the end.
-// Operands stream through a buffer LDS-DMA ring of 32-deep K-steps (64 B per row).
+// lane kernel: waves arranged WR (along corpus rows) x WQ (along queries); each wave owns NB
+// 32-row blocks x BJ 32-query blocks of the workgroup tile (MFMA 32x32: corpus rows are the A
+// operand, queries B), so every lane's accumulator columns are BJ queries and the lane keeps
+// one partial top-k list per query in registers. The epilogue is lane-local: per 16-row group a
+// max and a compare with the lane's threshold for that query; only groups that reach it are
+// scanned (staged through a per-lane LDS slot) and inserted. No candidate buffers, atomics or
+// barriers, so nothing in the epilogue waits on another wave, and with two workgroups per CU
+// one workgroup's epilogue runs beside the other's MFMAs. The 2 * WR partial lists of a query
+// (row-waves x lane halves hold disjoint rows) merge once, at the end.
+// Operands stream through a buffer LDS-DMA ring of STAGES 32-deep K-steps (64 B per row) that
+// runs ahead across corpus-tile boundaries.
 // =============================================================================================
 namespace lanek {
 constexpr int kRowBytes = 64;  // one k-tile of one row: 4 chunks of 16 B
 
-template <int NB, int WAVES, int STAGES>
+template <int NB, int BJ, int WR, int WQ, int STAGES>
 struct Cfg {
-  static constexpr int kThreads = WAVES * 64;
-  static constexpr int kTileRows = 32 * NB;
-  static constexpr int kTileQ = 32 * WAVES;
+  static constexpr int kWaves = WR * WQ;
+  static constexpr int kThreads = kWaves * 64;
+  static constexpr int kTileRows = 32 * NB * WR;
+  static constexpr int kTileQ = 32 * BJ * WQ;
+  static constexpr int kParts = 2 * WR;  // partial lists per query
   static constexpr int kStageBytes = (kTileRows + kTileQ) * kRowBytes;
-  static constexpr int kLoadsPerWave = (kTileRows + kTileQ) / 16 / WAVES;  // 1-KiB DMA instructions
+  static constexpr int kLoadsPerWave = (kTileRows + kTileQ) / 16 / kWaves;  // 1-KiB DMA instructions
   static constexpr int kLdsBytes = STAGES * kStageBytes;          // operand ring
   static constexpr int kLdsTotal = kLdsBytes + kThreads * 64;     // + one 16-score slot per lane
-  static_assert((kTileRows + kTileQ) % (16 * WAVES) == 0, "tile rows must split evenly over waves");
-  static_assert(kTileRows % (16 * WAVES) == 0, "corpus rows must split evenly over waves");
+  static_assert((kTileRows + kTileQ) % (16 * kWaves) == 0, "tile rows must split evenly over waves");
   static_assert(kLdsTotal <= 160 * 1024, "lane kernel LDS exceeds 160 KiB");
-  static_assert(WAVES * 64 * 16 * 8 <= kLdsTotal, "final list exchange (KCAP <= 16) must fit");
+  static_assert(kTileQ * kParts * 16 * 8 <= kLdsTotal, "final list exchange (KCAP <= 16) must fit");
+  static_assert(NB * BJ <= 32, "group mask is 32 bits");
 };
 
 // 64-B rows: a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the row so the 16
@@ -640,22 +646,24 @@ __device__ __forceinline__ int swz(int row, int chunk) {
 }
 }  // namespace lanek
 
-template <int DT, int KCAP, int NB, int WAVES, int STAGES, int MINB>
-__global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
+template <int DT, int KCAP, int NB, int BJ, int WR, int WQ, int STAGES, int MINB>
+__global__ __launch_bounds__(WR * WQ * 64, MINB) void topk_lane_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
     int n_rows, int n_q, int n_ktiles, int n_splits, int n_row_tiles, uint32_t row_base, int k_out,
     uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int qblocks, int flags) {
-  using C = lanek::Cfg<NB, WAVES, STAGES>;
+  using C = lanek::Cfg<NB, BJ, WR, WQ, STAGES>;
   using lanek::kRowBytes;
   using lanek::swz;
   constexpr int TR = C::kTileRows;
   constexpr int TQ = C::kTileQ;
   constexpr int LPW = C::kLoadsPerWave;
-  constexpr int LPW_C = TR / 16 / WAVES;  // of which corpus rows
+  constexpr int P = C::kParts;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave % WR;
+  const int wq = wave / WR;
   const int fr = lane & 31;
   const int fh = lane >> 5;
   int split, qb;
@@ -673,28 +681,31 @@ __global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
   const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
   const int total = (t_end - t_begin) * n_ktiles;
 
-  // this lane's query and its threshold: seed from the pre-pass, then the list's k-th key
-  const int q = q0 + wave * 32 + fr;
-  const bool q_ok = q < n_q;
-  float thr = q_ok ? ((thr_init) ? thr_init[q] : -INFINITY) : INFINITY;
-  uint64_t thk = (q_ok && thr != -INFINITY) ? (((uint64_t)ord_f32(thr) << 32) - 1) : 0;
-  const uint64_t thk_seed = thk;
-  uint64_t L[KCAP];
+  // this lane's BJ queries, their thresholds (pre-pass seed, then the list's k-th key) and lists
+  float thr[BJ];
+  uint64_t thk[BJ];
+  uint64_t L[BJ][KCAP];
 #pragma unroll
-  for (int j = 0; j < KCAP; ++j) L[j] = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init read retired before the ring counts
+  for (int bj = 0; bj < BJ; ++bj) {
+    const int q = q0 + wq * BJ * 32 + bj * 32 + fr;
+    thr[bj] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+    thk[bj] = (q < n_q && thr[bj] != -INFINITY) ? (((uint64_t)ord_f32(thr[bj]) << 32) - 1) : 0;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[bj][j] = 0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init reads retired before the ring counts
 
-  // ---- operand ring: wave w moves LPW_C 1-KiB pieces of the corpus tile and LPW - LPW_C of the
-  // query tile; lane l of a piece lands at (row 16p + l/4, physical chunk l%4).
+  // ---- operand ring: the workgroup's (TR + TQ) / 16 1-KiB pieces per K-step, LPW per wave;
+  // corpus pieces first (LDS rows 0..TR-1), then query pieces; lane l of a piece lands at
+  // (row 16p + l/4, physical chunk l%4) and loads the logical chunk (l%4) ^ swz(row).
   const int ld_row = lane >> 2;
   const uint32_t c_bytes = (uint32_t)(TR * row_stride);
   const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, (uint32_t)(TQ * row_stride));
   uint32_t ld_off[LPW];
 #pragma unroll
   for (int j = 0; j < LPW; ++j) {
-    const int piece = wave * LPW + j;  // 0 .. (TR+TQ)/16 - 1 over the workgroup
-    const int prow = (piece < TR / 16) ? piece * 16 : (piece - TR / 16) * 16;
-    const int row = prow + ld_row;
+    const int piece = wave * LPW + j;
+    const int row = ((piece < TR / 16) ? piece * 16 : (piece - TR / 16) * 16) + ld_row;
     ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 3) ^ ((row >> 2) & 3)) << 4);
   }
   auto issue = [&](int s) {
@@ -705,7 +716,6 @@ __global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int piece = wave * LPW + j;
-      // corpus pieces first (rows 0..TR-1), then query pieces (LDS rows TR..TR+TQ-1)
       blds16(piece < TR / 16 ? c_rsrc : q_rsrc, ld_off[j] + kt * kRowBytes, buf + piece * 16 * kRowBytes);
     }
   };
@@ -713,11 +723,11 @@ __global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
   for (int i = 0; i < STAGES - 1; ++i)
     if (i < total) issue(i);
 
-  f32x16 acc[NB];
-  const int row_l = 4 * fh;  // + bi*32 + (r&3) + 8*(r>>2)
-  // per-lane 64-B slot after the operand ring: a passing 16-row group is staged here so the
-  // scan reads its scores with lane-varying LDS addresses instead of register select chains
-  float* slot = reinterpret_cast<float*>(smem + C::kLdsBytes) + (wave * 64 + lane) * 16;
+  f32x16 acc[NB][BJ];
+  const int row_w = wr * NB * 32 + 4 * fh;  // + bi*32 + (r&3) + 8*(r>>2)
+  // per-lane 64-B slot after the operand ring: a passing 16-row group is staged here so the scan
+  // reads its scores with lane-varying LDS addresses instead of register select chains
+  float* slot = reinterpret_cast<float*>(smem + C::kLdsBytes) + tid * 16;
 
   const bool skip_epilogue = (flags & kFlagSkipEpilogue) != 0;
   for (int s = 0; s < total; ++s) {
@@ -747,135 +757,163 @@ __global__ __launch_bounds__(WAVES * 64, MINB) void topk_lane_kernel(
 #pragma unroll
       for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[bi][r] = 0.f;
+        for (int bj = 0; bj < BJ; ++bj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.f;
     }
     const unsigned char* buf = smem + (s % STAGES) * C::kStageBytes;
-    // Fragment schedule: the NB + 1 reads of k16 step 0, then step 0's MFMAs each paired with
-    // one read of step 1, then step 1's MFMAs. Reads stay ahead of their MFMAs (counted
-    // lgkmcnt waits, at most 15 outstanding: the counter's width) instead of the compiler's
+    // Fragment schedule: the NB + BJ reads of k16 step 0, then step 0's MFMAs interleaved with
+    // the reads of step 1, then step 1's MFMAs. Reads stay ahead of their MFMAs (counted lgkmcnt
+    // waits, at most 15 outstanding: the counter's width) instead of the compiler's
     // register-saving order, where every MFMA waits out an LDS latency.
-    u32x4 fb[2], fa[2][NB];
+    u32x4 fa[2][NB], fb[2][BJ];
     auto frag_reads = [&](int g) __attribute__((always_inline)) {
       const int ch = 2 * g + fh;
-      fb[g] = *reinterpret_cast<const u32x4*>(buf + TR * kRowBytes + swz(wave * 32 + fr, ch));
 #pragma unroll
-      for (int bi = 0; bi < NB; ++bi) fa[g][bi] = *reinterpret_cast<const u32x4*>(buf + swz(bi * 32 + fr, ch));
+      for (int bj = 0; bj < BJ; ++bj)
+        fb[g][bj] = *reinterpret_cast<const u32x4*>(buf + TR * kRowBytes + swz(wq * BJ * 32 + bj * 32 + fr, ch));
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi)
+        fa[g][bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * NB * 32 + bi * 32 + fr, ch));
     };
     frag_reads(0);
     __builtin_amdgcn_sched_barrier(0);
     frag_reads(1);
 #pragma unroll
-    for (int bi = 0; bi < NB; ++bi) mfma_step<DT>(fa[0][bi], fb[0], acc[bi]);
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < BJ; ++bj) mfma_step<DT>(fa[0][bi], fb[0][bj], acc[bi][bj]);
     if constexpr (DT != DT_F32) {  // f32 steps are 4 MFMAs each: leave those to the scheduler
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+      for (int i = 0; i < (NB * BJ > NB + BJ ? NB * BJ : NB + BJ); ++i) {
+        if (i < NB * BJ) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        if (i < NB + BJ) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
       }
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int bi = 0; bi < NB; ++bi) mfma_step<DT>(fa[1][bi], fb[1], acc[bi]);
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < BJ; ++bj) mfma_step<DT>(fa[1][bi], fb[1][bj], acc[bi][bj]);
     __builtin_amdgcn_sched_barrier(0);
     if (kt != n_ktiles - 1 || skip_epilogue) continue;
-    // ---- lane-local epilogue of corpus tile t_begin + tk
+
     const int r0 = (t_begin + tk) * TR;
-    uint32_t gmask = 0;  // 16-row groups whose max reaches the threshold
+    // ---- lane-local epilogue of corpus tile t_begin + tk: groups (bi, bj) whose max reaches
+    // the threshold of query bj
+    uint32_t gmask = 0;
 #pragma unroll
-    for (int bi = 0; bi < NB; ++bi) {
-      float m0 = acc[bi][0], m1 = acc[bi][1];
+    for (int bj = 0; bj < BJ; ++bj)
 #pragma unroll
-      for (int r = 2; r < 16; r += 2) {
-        m0 = fmaxf(m0, acc[bi][r]);
-        m1 = fmaxf(m1, acc[bi][r + 1]);
+      for (int bi = 0; bi < NB; ++bi) {
+        float m0 = acc[bi][bj][0], m1 = acc[bi][bj][1];
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+          m0 = fmaxf(m0, acc[bi][bj][r]);
+          m1 = fmaxf(m1, acc[bi][bj][r + 1]);
+        }
+        gmask |= (fmaxf(m0, m1) >= thr[bj] ? 1u : 0u) << (bj * NB + bi);
       }
-      gmask |= (fmaxf(m0, m1) >= thr ? 1u : 0u) << bi;
-    }
     if (flags & kFlagMaxOnly) {
       if (gmask == 0xFFFFFFFFu) part_keys[0] = 1;  // keep the maxima live
       continue;
     }
     // One passing group per lane per round: stage it (a static branch per group, taken only
-    // where some lane selected it), build its pass mask, then one list_insert per passing score
-    // in a divergent loop: the wave pays max-survivors-per-lane inserts.
+    // where some lane selected it), build its pass mask, then one list_insert per passing
+    // score in a divergent loop: the wave pays max-survivors-per-lane inserts.
     while (__ballot(gmask != 0)) {
       const int sel = gmask ? __builtin_ctz(gmask) : -1;
       gmask &= gmask - 1;
 #pragma unroll
-      for (int bi = 0; bi < NB; ++bi) {
-        if (sel == bi) {
+      for (int bj = 0; bj < BJ; ++bj)
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi) {
+          if (sel == bj * NB + bi) {
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+              f32x4 v4 = {acc[bi][bj][4 * c4], acc[bi][bj][4 * c4 + 1], acc[bi][bj][4 * c4 + 2],
+                          acc[bi][bj][4 * c4 + 3]};
+              *reinterpret_cast<f32x4*>(slot + 4 * c4) = v4;
+            }
+          }
+        }
+      if (sel >= 0) {
+        const int bjs = sel / NB;
+        const int rb = r0 + row_w + (sel - bjs * NB) * 32;
+#pragma unroll
+        for (int bj = 0; bj < BJ; ++bj) {
+          if (bjs != bj) continue;
+          uint32_t pm = 0;
 #pragma unroll
           for (int c4 = 0; c4 < 4; ++c4) {
-            f32x4 v4 = {acc[bi][4 * c4], acc[bi][4 * c4 + 1], acc[bi][4 * c4 + 2], acc[bi][4 * c4 + 3]};
-            *reinterpret_cast<f32x4*>(slot + 4 * c4) = v4;
-          }
-        }
-      }
-      if (sel >= 0) {
-        const int rb = r0 + sel * 32 + row_l;
-        uint32_t pm = 0;
+            const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
 #pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * c4 + e;
-            pm |= (v4[e] >= thr && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * c4 + e;
+              pm |= (v4[e] >= thr[bj] && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
+            }
           }
-        }
-        bool ins = false;
-        while (pm) {
-          const int r = __builtin_ctz(pm);
-          pm &= pm - 1;
-          const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
-          if (key > thk) {
-            list_insert<KCAP>(L, key);
-            ins = true;
+          bool ins = false;
+          while (pm) {
+            const int r = __builtin_ctz(pm);
+            pm &= pm - 1;
+            const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
+            if (key > thk[bj]) {
+              list_insert<KCAP>(L[bj], key);
+              ins = true;
+            }
           }
-        }
-        if (ins) {
-          const uint64_t kth = list_at<KCAP>(L, k_out - 1);
-          if (kth > thk) {
-            thk = kth;
-            thr = key_score(kth);
+          if (ins) {
+            const uint64_t kth = list_at<KCAP>(L[bj], k_out - 1);
+            if (kth > thk[bj]) {
+              thk[bj] = kth;
+              thr[bj] = key_score(kth);
+            }
           }
         }
       }
     }
   }
-
   if (skip_epilogue) {
     float sink = 0.f;
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sink += acc[bi][r];
+      for (int bj = 0; bj < BJ; ++bj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
     if (sink == 1234.5678f) part_keys[0] = 1;
     return;
   }
 
-  // ---- merge the two half-wave lists of each query (lanes l, l+32) through LDS, then write
+  // ---- merge the P partial lists of each query (row-waves x lane halves) through LDS
   __syncthreads();  // every wave is done with the operand ring (all DMA retired at the last step)
-  uint64_t* xl = reinterpret_cast<uint64_t*>(smem) + (wave * 64 + lane) * KCAP;
+  uint64_t* xl = reinterpret_cast<uint64_t*>(smem);
+  const int part = wr * 2 + fh;
 #pragma unroll
-  for (int j = 0; j < KCAP; ++j) xl[j] = L[j];
-  __builtin_amdgcn_wave_barrier();
-  if (fh == 0) {
-    const uint64_t* pl = xl + 32 * KCAP;  // partner lane l + 32
-    for (int j = 0; j < KCAP; ++j) {
-      const uint64_t kk = pl[j];
-      if (kk == 0 || kk <= L[KCAP - 1]) break;  // sorted: nothing further can enter
-      list_insert<KCAP>(L, kk);
-    }
-    if (q_ok) {
-      uint64_t* dst = part_keys + ((int64_t)q * n_splits + split) * k_out;
+  for (int bj = 0; bj < BJ; ++bj) {
+    const int ql = wq * BJ * 32 + bj * 32 + fr;
 #pragma unroll
-      for (int j = 0; j < KCAP; ++j)
-        if (j < k_out) dst[j] = L[j];
-    }
+    for (int j = 0; j < KCAP; ++j) xl[(ql * P + part) * KCAP + j] = L[bj][j];
   }
-  (void)thk_seed;
+  __syncthreads();
+  if (tid < TQ && q0 + tid < n_q) {
+    uint64_t M[KCAP];
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) M[j] = xl[(tid * P) * KCAP + j];
+    for (int u = 1; u < P; ++u) {
+      const uint64_t* src = xl + (tid * P + u) * KCAP;
+      for (int j = 0; j < KCAP; ++j) {
+        const uint64_t kk = src[j];
+        if (kk <= M[KCAP - 1]) break;  // sorted: nothing further can enter
+        list_insert<KCAP>(M, kk);
+      }
+    }
+    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j)
+      if (j < k_out) dst[j] = M[j];
+  }
 }
 
 // Merge n_lists sorted key lists per query into the top k. One wave per query: every lane
@@ -1184,8 +1222,12 @@ constexpr int kResidentSlotsV1 = 256 * 2;
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_V1;
-  if (k <= 16 && B >= kWideMinBatch && !(ix->debug_flags & kFlagTile128))
-    p.kernel = (ix->debug_flags & kFlagLane256q128) ? KERNEL_LANE256Q128 : KERNEL_LANE256;
+  if (k <= 16 && !(ix->debug_flags & kFlagTile128)) {
+    if (ix->debug_flags & kFlagLane256q128)
+      p.kernel = KERNEL_LANE256Q128;
+    else if (B >= kWideMinBatch)
+      p.kernel = KERNEL_LANE256;
+  }
   if (p.kernel != KERNEL_V1) {
     // Row tile TR, query tile TQ, `per_cu` resident workgroups per CU. One wave of workgroups;
     // splits a multiple of 8 (rounded down: an extra workgroup would run as a second wave) so
@@ -1270,28 +1312,32 @@ void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_s
                      n_splits, qblocks, flags);
 }
 
-template <int DT, int KCAP, int NB, int WAVES, int STAGES, int MINB>
+template <int DT, int KCAP, int NB, int BJ, int WR, int WQ, int STAGES, int MINB>
 void launch_lane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                  const float* thr, int flags, hipStream_t s) {
-  using C = lanek::Cfg<NB, WAVES, STAGES>;
+  using C = lanek::Cfg<NB, BJ, WR, WQ, STAGES>;
+  constexpr auto kern = &topk_lane_kernel<DT, KCAP, NB, BJ, WR, WQ, STAGES, MINB>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_lane_kernel<DT, KCAP, NB, WAVES, STAGES, MINB>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsTotal);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C::kLdsTotal);
     attr_set = true;
   }
-  hipLaunchKernelGGL((topk_lane_kernel<DT, KCAP, NB, WAVES, STAGES, MINB>), dim3((unsigned)(p.n_splits * p.qblocks)),
-                     dim3(C::kThreads), C::kLdsTotal, s, ix->rows, ix->qbuf, ix->row_stride, n_rows, B,
-                     ix->d_pad * ix->elem / lanek::kRowBytes, p.n_splits, p.n_row_tiles, row_base, k, ix->part, thr,
-                     p.qblocks, flags);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(C::kThreads), C::kLdsTotal, s, ix->rows,
+                     ix->qbuf, ix->row_stride, n_rows, B, ix->d_pad * ix->elem / lanek::kRowBytes, p.n_splits,
+                     p.n_row_tiles, row_base, k, ix->part, thr, p.qblocks, flags);
 }
 
-template <int DT, int NB, int WAVES, int STAGES, int MINB>
-void launch_lane_k(int kc, const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+// lane lists sized to k: 8, 12 or 16 keys (insert and select cost scale with the size)
+template <int DT, int NB, int BJ, int WR, int WQ, int STAGES, int MINB>
+void launch_lane_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                    const float* thr, int flags, hipStream_t s) {
-  if (kc == 8) launch_lane<DT, 8, NB, WAVES, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
-  else if (kc == 12) launch_lane<DT, 12, NB, WAVES, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
-  else launch_lane<DT, 16, NB, WAVES, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  if (k <= 8)
+    launch_lane<DT, 8, NB, BJ, WR, WQ, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  else if (k <= 12)
+    launch_lane<DT, 12, NB, BJ, WR, WQ, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  else
+    launch_lane<DT, 16, NB, BJ, WR, WQ, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
 }
 
 template <int DT>
@@ -1313,13 +1359,12 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
-  if (p.kernel != KERNEL_V1) {
-    // lane lists sized to k: 8, 12 or 16 keys (insert and select cost scale with the size)
-    const int kc = k <= 8 ? 8 : (k <= 12 ? 12 : 16);
-    if (p.kernel == KERNEL_LANE256Q128)
-      launch_lane_k<DT, 8, 4, 2, 2>(kc, ix, p, n, B, k, row_base, thr, flags, s);
-    else
-      launch_lane_k<DT, 8, 8, 4, 1>(kc, ix, p, n, B, k, row_base, thr, flags, s);
+  if (p.kernel == KERNEL_LANE256Q128) {
+    launch_lane_k<DT, 8, 1, 1, 4, 2, 2>(ix, p, n, B, k, row_base, thr, flags, s);
+    return;
+  }
+  if (p.kernel == KERNEL_LANE256) {
+    launch_lane_k<DT, 8, 1, 1, 8, 4, 1>(ix, p, n, B, k, row_base, thr, flags, s);
     return;
   }
   switch (k <= 8 ? 8 : (k <= 12 ? 12 : (k <= 16 ? 16 : 32))) {  // lists sized to k
@@ -1567,7 +1612,7 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kKernelFlags);
+  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kKernelFlags);
   return AHR_OK;
 }
 

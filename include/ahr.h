@@ -99,10 +99,10 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_c
 /* Rows scored by the threshold pre-pass (0 disables it; else a power of two in [128, 1024]). */
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
-/* Ablation switches for profiling, never set in production: 2 = skip the top-k epilogue (GEMM
- * cost only, results are garbage); 8 = always the 128x128 tile kernel; 64 = lane kernel with a
- * 256x128 workgroup tile; 256 = lane kernel epilogue stops after the group maxima (garbage).
- * 8 and 64 give correct results. */
+/* Ablation switches for profiling, never set in production. Correct results: 8 = always the
+ * 128x128 tile kernel, 64 = the 256x128 lane kernel (k <= 16). Garbage results (cost splits):
+ * 2 = skip the top-k epilogue, 256 = lane epilogue stops after the group maxima, 512 = tile
+ * kernel loads operands for its first tile only. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
