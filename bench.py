@@ -93,12 +93,15 @@ def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float)
                        f"{dt:.1f}s; host os.cpu_count()={os.cpu_count()}")}
 
 
-def read_traffic(kernel: str, launches_per_step: int = 1):
-    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), if any."""
+def read_traffic(kernel: str, workload: str, batch: int):
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), if it was
+    measured on this workload and batch (else None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             data = json.load(f)
+        if data.get("_workload", "hotpot90k") != workload or data.get("_batch", 1024) != batch:
+            return None
         return data.get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -238,7 +241,7 @@ def main() -> None:
                 "peak": peak,
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / peak, 4),
-                "traffic": read_traffic(kname),
+                "traffic": read_traffic(kname, args.workload, B),
                 "algorithmic_flops_per_launch": flops,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "hbm_equiv_GBs": round(alg_bytes / (tile_ms * 1e-3) / 1e9, 1),

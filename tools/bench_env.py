@@ -1,0 +1,151 @@
+"""C5 benchmark: 2-hop expand + re-score inside the RL environment loop (SURVEY §8, configs[4]).
+
+Builds a HotpotQA-distractor-shaped graph (87,000 entities + 3,000 summaries indexed,
+2 belongs_to parents per entity, ~2 related_to per summary, 40,000 hyperedges x ~3.8
+participants, unindexed) with the seeded corpus vectors of ah_rag.synthetic written straight into
+the vector store (no encoder weights offline), then times
+  * vec:    VecAHRAGGymEnv with E environments: one batched reset (dense top-5 + expansion +
+            rerank for all E queries) and `steps` batched steps of random valid actions;
+  * single: the drop-in AHRAGGymEnv stepped one environment at a time (B = 1 per call), the
+            reference's own loop shape (policy_ppo.py:145,163-214) on the device graph.
+Replicas per GPU: one process per GPU, environments partitioned; no collective.
+Prints one JSON line. Usage: python tools/bench_env.py [--envs 1024] [--steps 6]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ah-rag_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ah_rag.agent.gym_env import AHRAGGymEnv  # noqa: E402
+from ah_rag.agent.vec_env import VecAHRAGGymEnv  # noqa: E402
+from ah_rag.graph.hierarchical_graph import HierarchicalGraph, VectorStore  # noqa: E402
+from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus  # noqa: E402
+
+
+def build_graph(corpus: SyntheticCorpus, rng: np.random.Generator, n_hyper: int = 40_000):
+    s = corpus.spec
+    topics = corpus.topics.numpy()
+    hg = HierarchicalGraph()
+    sids = [hg.add_summary(t, title=f"Topic {t}", summary_text=f"summary of topic {t}",
+                           confidence=float(rng.uniform(5, 10)), top_words=[f"w{t}", f"v{t}"],
+                           judge_scores={"overall": float(rng.uniform(0, 10))}) for t in range(s.n_summaries)]
+    eids = [hg.add_entity(f"entity {i}", description=f"entity {i} of topic {topics[i]}", entity_type="thing")
+            for i in range(s.n_entities)]
+    second = rng.integers(0, s.n_summaries, s.n_entities)
+    for i, e in enumerate(eids):
+        hg.add_belongs_to(e, sids[topics[i] % s.n_summaries], prob=0.9)
+        if second[i] != topics[i] % s.n_summaries:
+            hg.add_belongs_to(e, sids[second[i]], prob=0.1)
+    for t in range(s.n_summaries):
+        for u in rng.integers(0, s.n_summaries, 2):
+            if u != t:
+                hg.add_related(sids[t], sids[u], weight=0.5)
+    by_topic = {}
+    for i, t in enumerate(topics):
+        by_topic.setdefault(int(t), []).append(i)
+    for h in range(n_hyper):
+        pool = by_topic[int(rng.integers(0, s.n_centroids))]
+        k = min(len(pool), int(rng.integers(2, 6)))  # mean ~3.5-3.8 participants
+        hid = hg.add_hyperedge(f"h{h}", description=f"relation {h}", relation_type="rel",
+                               confidence_score=float(rng.uniform(0, 1)))
+        for i in rng.choice(pool, k, replace=False):
+            hg.add_participation(eids[int(i)], hid)
+    return hg, eids + sids
+
+
+def install_vectors(hg: HierarchicalGraph, ids, vectors: np.ndarray, db_path: str) -> None:
+    """What build_vector_index stores, with the corpus vectors instead of an encoder's."""
+    store = VectorStore(db_path)
+    store.clear()
+    metas = [hg._embedding_text(n)[1] for n in ids]
+    store.upsert(ids, vectors, metas)
+    store.save("synthetic")
+    hg.G.graph["vector_index"] = {"db_path": db_path, "model": "synthetic", "indexed_nodes": len(ids),
+                                  "indexed_meta": {n: hg._index_key(hg.G.nodes[n]) for n in ids}}
+    hg.G.graph["dirty"] = False
+
+
+def random_actions(rng, masks):
+    return [int(rng.choice(np.flatnonzero(np.asarray(m)))) for m in masks]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--single", type=int, default=32, help="environments stepped one by one")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(20251003)
+    t0 = time.perf_counter()
+    corpus = SyntheticCorpus(HOTPOT_90K, dev)
+    vectors = corpus.rows().cpu().numpy()
+    hg, ids = build_graph(corpus, rng)
+    tmp = tempfile.mkdtemp(prefix="ahr_env_")
+    install_vectors(hg, ids, vectors, os.path.join(tmp, "vector_db"))
+    q, _ = corpus.queries(a.envs, corpus.rows())
+    qv = q.cpu().numpy()
+    queries = [f"query {i}" for i in range(a.envs)]
+    t_build = time.perf_counter() - t0
+
+    venv = VecAHRAGGymEnv(n_envs=a.envs, max_steps=a.steps + 1, graph=hg)
+    # warm-up episode: device graph, index, expansion kernels, host caches
+    venv.reset(queries[:a.envs], query_vectors=qv)
+    for _ in range(a.steps):
+        venv.step(random_actions(rng, [e.get_action_mask() for e in venv.envs]))
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    venv.reset(queries, query_vectors=qv)
+    t_reset = time.perf_counter() - t1
+    step_times = []
+    for _ in range(a.steps):
+        masks = [e.get_action_mask() for e in venv.envs]
+        acts = random_actions(rng, masks)
+        ts = time.perf_counter()
+        venv.step(acts)
+        step_times.append(time.perf_counter() - ts)
+    vec_steps = a.envs * (1 + a.steps)
+    vec_time = t_reset + sum(step_times)
+
+    # single-environment loop (B = 1 per search / expansion), a subset of the same queries
+    n1 = min(a.single, a.envs)
+    env = AHRAGGymEnv(max_steps=a.steps + 1, graph=hg)
+    env.env.logging_enabled = False
+    # one search first so the device graph / index are warm
+    hg.search_batch(queries[:1], top_k=5, return_cluster=True, query_vectors=qv[:1])
+    ts = time.perf_counter()
+    for i in range(n1):
+        # reset with a precomputed vector: the same path VecAHRAGGymEnv uses, at B = 1
+        sub = VecAHRAGGymEnv.__new__(VecAHRAGGymEnv)
+        sub.hg, sub.envs = hg, [env]
+        sub.reset([queries[i]], query_vectors=qv[i:i + 1])
+        for _ in range(a.steps):
+            env.step(random_actions(rng, [env.get_action_mask()])[0])
+    single_time = time.perf_counter() - ts
+    step_only = a.envs * a.steps / sum(step_times)
+    single_steps = n1 * (1 + a.steps)
+
+    out = {
+        "metric": "env steps/sec (reset + steps, 2-hop expand + rerank), C5 on 1 MI355X",
+        "envs": a.envs, "steps_per_episode": a.steps,
+        "vec_env_steps_per_s": round(vec_steps / vec_time, 1),
+        "vec_step_only_per_s": round(step_only, 1),
+        "vec_reset_ms": round(t_reset * 1e3, 2), "vec_step_ms": [round(t * 1e3, 2) for t in step_times],
+        "single_env_steps_per_s": round(single_steps / single_time, 1), "single_envs": n1,
+        "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
+        "build_s": round(t_build, 1),
+        "data": "synthetic HotpotQA-distractor-shaped graph (SURVEY §8d), seeded corpus vectors, random valid actions",
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

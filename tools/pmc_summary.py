@@ -55,6 +55,8 @@ def durations(pattern: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("pmc_dir")
+    ap.add_argument("--workload", default="hotpot90k", help="bench workload the passes ran (bench reads only a match)")
+    ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                    "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
@@ -64,7 +66,7 @@ def main() -> None:
     dur = durations(os.path.join(a.pmc_dir, "trace", "*", "*_kernel_stats.csv"))
     out = {"_method": ("FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction) + WRITE_SIZE KiB x 1024, "
                        "mean per launch, separate rocprofv3 --pmc passes; durations from --kernel-trace --stats"),
-           "_source": a.pmc_dir}
+           "_source": a.pmc_dir, "_workload": a.workload, "_batch": a.batch}
     for k in sorted(set(fetch) | set(write) | set(dur)):
         base = k.split("<")[0]
         if base not in ("topk_tile_kernel", "topk_lane_kernel", "merge_lane_lists_kernel", "merge_heads_kernel",
