@@ -1,0 +1,40 @@
+"""L1 topic relations on the GPU (centroid cosine as one fp32 GEMM) vs the reference outputs.
+
+Tolerance: the GPU fp32 dot products may differ from numpy's float32 np.dot in the last bits, so
+cosine/weight are compared within 1e-4 after the reference's 4-dp rounding, and a pair may only
+differ in membership when its reference cosine lies within 1e-5 of the cosine threshold.
+Everything else (pair order, overlap, jaccard, confidence, top-k, neighbour ids) is exact.
+"""
+import copy
+import json
+import os
+
+import pytest
+
+from ah_rag.aggregate import relations as rel
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "relations_cases.json")
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_gpu_relations_match_reference(cuda, tmp_path, case):
+    with open(GOLDEN, encoding="utf-8") as f:
+        g = json.load(f)
+    c = g["cases"][case]
+    nodes = copy.deepcopy(g["l1_nodes"])
+    edges = rel.generate_l1_relations(nodes, artifact_dir=str(tmp_path), device=cuda, **c["params"])
+    thr = c["params"].get("min_cosine", 0.5)
+    want = {(e["source"], e["target"]): e for e in c["edges"]}
+    got = {(e["source"], e["target"]): e for e in edges}
+    for key in set(want) ^ set(got):
+        e = want.get(key) or got.get(key)
+        assert abs(e["cosine"] - thr) < 1e-4, key
+    common = [k for k in [(e["source"], e["target"]) for e in c["edges"]] if k in got]
+    assert common == [k for k in [(e["source"], e["target"]) for e in edges] if k in want]  # same order
+    for k in common:
+        a, b = want[k], got[k]
+        assert (a["overlap"], a["jaccard"], a["confidence"], a["relation_type"]) == \
+               (b["overlap"], b["jaccard"], b["confidence"], b["relation_type"])
+        assert abs(a["cosine"] - b["cosine"]) <= 1e-4 + 1e-12
+        assert abs(a["weight"] - b["weight"]) <= 1e-4 + 1e-12
