@@ -203,7 +203,7 @@ class DenseIndex:
         8 = 128x128 tile kernel, 64 = 256x128 lane kernel, 256 = group maxima only (garbage)."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
-    _KERNELS = ("tile128", "lane256", "lane256x128")
+    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

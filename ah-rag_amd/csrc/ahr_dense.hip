@@ -76,6 +76,9 @@ static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
 __device__ __forceinline__ int swz(int row, int chunk) {
   return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
+// 64-B rows (half k-tiles): a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the
+// row so the 16 rows of a ds_read_b128 lane group hit 16 distinct 16-B slots.
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
 // Sorted (descending) register list of packed keys; drops the smallest on insert.
 template <int KCAP>
@@ -176,12 +179,13 @@ enum { MODE_TOPK = 0, MODE_GROUPMAX = 1 };
 enum {
   kFlagXcdRemap = 1,
   kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
-  kFlagTile128 = 8,       // always the 128x128 tile kernel
+  kFlagTile128 = 8,       // the 128x128 tile kernel with cooperative screening, any k
+  kFlagTileLane = 32,     // the 128x128 lane-local kernel at any batch (k <= 16)
   kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
   kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
   kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
 };
-constexpr int kKernelFlags = kFlagTile128 | kFlagLane256q128;
+constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
@@ -228,34 +232,19 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
   int* flag = reinterpret_cast<int*>(smem + kOffFlag);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + kOffCand);
 
-  // k <= 16: lane-local top-k (each lane keeps lists for its two query columns, screens its
-  // own scores; no LDS candidate buffers, no epilogue barriers). k > 16: cooperative screening
-  // into per-query LDS candidate lists folded by one owner thread per query.
-  constexpr bool LANE = MODE == MODE_TOPK && KCAP <= 16;
+  // Cooperative screening into per-query LDS candidate lists folded by one owner thread per
+  // query (k > 16; k <= 16 has the lane-local topk_tilelane_kernel).
   uint64_t L[KCAP];
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) L[j] = 0;
-  uint64_t LL[2][LANE ? KCAP : 1];
-  float lthr[2];
-  uint64_t lthk[2];
-  if constexpr (LANE) {
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) {
-#pragma unroll
-      for (int j = 0; j < KCAP; ++j) LL[bj][j] = 0;
-      const int q = q0 + wq * 64 + bj * 32 + fr;
-      lthr[bj] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
-      lthk[bj] = (q < n_q && lthr[bj] != -INFINITY) ? (((uint64_t)ord_f32(lthr[bj]) << 32) - 1) : 0;
-    }
-  }
-  if (!LANE && tid < kTileQ) {
+  if (tid < kTileQ) {
     // A row whose score equals the seed may still win on the row tie-break: the seed key is
     // the smallest key with that score, minus one.
     const float seed = (thr_init && q0 + tid < n_q) ? thr_init[q0 + tid] : -INFINITY;
     thr_score[tid] = seed;
     thr_key[tid] = seed == -INFINITY ? 0 : (((uint64_t)ord_f32(seed) << 32) - 1);
   }
-  if (!LANE && tid < 2) flag[tid] = 0;
+  if (tid < 2) flag[tid] = 0;
 
   // Staging by global_load_lds (no staging registers): wave w fills rows [32w, 32w+32) of both
   // tiles, 8 rows (1 KiB) per instruction; lane l lands at (row 8j + l/8, physical chunk l%8) and
@@ -353,83 +342,6 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
       }
       __syncthreads();
       continue;
-    }
-
-    if constexpr (LANE) {
-      if (!(flags & kFlagSkipEpilogue)) {
-        // 16-row groups (bi, bj) whose max reaches the column's threshold; one group per lane
-        // per round is staged into the lane's 64-B slot in the second staging buffer (idle
-        // here: the next tile refills it only after the barrier behind its first stage, which
-        // every wave reaches after its epilogue) and scanned from there.
-        uint32_t gmask = 0;
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-          for (int bi = 0; bi < 2; ++bi) {
-            float m0 = acc[bi][bj][0], m1 = acc[bi][bj][1];
-#pragma unroll
-            for (int r = 2; r < 16; r += 2) {
-              m0 = fmaxf(m0, acc[bi][bj][r]);
-              m1 = fmaxf(m1, acc[bi][bj][r + 1]);
-            }
-            gmask |= (fmaxf(m0, m1) >= lthr[bj] ? 1u : 0u) << (bj * 2 + bi);
-          }
-        float* slot = reinterpret_cast<float*>(smem + kOffBuf1) + tid * 16;
-        while (__ballot(gmask != 0)) {
-          const int sel = gmask ? __builtin_ctz(gmask) : -1;
-          gmask &= gmask - 1;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            if (sel == g) {
-#pragma unroll
-              for (int c4 = 0; c4 < 4; ++c4) {
-                f32x4 v4 = {acc[g & 1][g >> 1][4 * c4], acc[g & 1][g >> 1][4 * c4 + 1], acc[g & 1][g >> 1][4 * c4 + 2],
-                            acc[g & 1][g >> 1][4 * c4 + 3]};
-                *reinterpret_cast<f32x4*>(slot + 4 * c4) = v4;
-              }
-            }
-          }
-          if (sel >= 0) {
-            const int bjs = sel >> 1;
-            const int rb = (int)r0 + wr * 64 + (sel & 1) * 32 + 4 * fh;
-            const float th = bjs ? lthr[1] : lthr[0];
-            uint32_t pm = 0;
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-              const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int r = 4 * c4 + e;
-                pm |= (v4[e] >= th && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
-              }
-            }
-            while (pm) {
-              const int r = __builtin_ctz(pm);
-              pm &= pm - 1;
-              const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
-              if (bjs == 0) {
-                if (key > lthk[0]) list_insert<KCAP>(LL[0], key);
-              } else {
-                if (key > lthk[1]) list_insert<KCAP>(LL[1], key);
-              }
-            }
-            if (bjs == 0) {
-              const uint64_t kth = list_at<KCAP>(LL[0], k_out - 1);
-              if (kth > lthk[0]) {
-                lthk[0] = kth;
-                lthr[0] = key_score(kth);
-              }
-            } else {
-              const uint64_t kth = list_at<KCAP>(LL[1], k_out - 1);
-              if (kth > lthk[1]) {
-                lthk[1] = kth;
-                lthr[1] = key_score(kth);
-              }
-            }
-          }
-        }
-        continue;
-      }
     }
 
     if (flags & kFlagSkipEpilogue) {  // ablation: GEMM only, keep acc live, no top-k
@@ -568,42 +480,304 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
     }
   }
 
-  if constexpr (LANE) {
-    // merge the 4 partial lists of each query (2 row-waves x 2 lane halves) through LDS
-    __syncthreads();  // staging buffers idle: every wave is past its last K-step
-    uint64_t* xl = reinterpret_cast<uint64_t*>(smem);
-    const int part = wr * 2 + fh;
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) {
-      const int ql = wq * 64 + bj * 32 + fr;
-#pragma unroll
-      for (int j = 0; j < KCAP; ++j) xl[(ql * 4 + part) * KCAP + j] = LL[bj][j];
-    }
-    __syncthreads();
-    if (tid < kTileQ && q0 + tid < n_q) {
-      uint64_t M[KCAP];
-#pragma unroll
-      for (int j = 0; j < KCAP; ++j) M[j] = xl[(tid * 4) * KCAP + j];
-      for (int u = 1; u < 4; ++u) {
-        const uint64_t* src = xl + (tid * 4 + u) * KCAP;
-        for (int j = 0; j < KCAP; ++j) {
-          const uint64_t kk = src[j];
-          if (kk <= M[KCAP - 1]) break;  // sorted: nothing further can enter
-          list_insert<KCAP>(M, kk);
-        }
-      }
-      uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
-#pragma unroll
-      for (int j = 0; j < KCAP; ++j)
-        if (j < k_out) dst[j] = M[j];
-    }
-  } else if (MODE == MODE_TOPK && tid < kTileQ && q0 + tid < n_q) {
+  if (MODE == MODE_TOPK && tid < kTileQ && q0 + tid < n_q) {
     uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
 #pragma unroll
     for (int j = 0; j < KCAP; ++j)
       if (j < k_out) dst[j] = L[j];
   }
 }
+
+// =============================================================================================
+// topk_tilelane_kernel (default for B < 6144, k <= 16): the 128x128 tile, 2x2 waves and K-loop
+// of topk_tile_kernel with a lane-local top-k. Each lane holds two query columns x 32 rows of a
+// tile; it keeps one sorted register list and one threshold per column (the pre-pass seed, then
+// the list's k-th key). At a tile's end: 16-row group maxima against the thresholds; lanes with
+// a passing group stage it into a private 64-B LDS slot (the second staging buffer is idle
+// there) and insert its passing scores, one list_insert per set bit of a pass mask in a
+// divergent loop. No candidate buffers, atomics or barriers; the other workgroup on the CU keeps
+// the MFMA pipe busy meanwhile. At the end the 4 partial lists of a query (2 row-waves x 2 lane
+// halves) merge through LDS.
+// (Measured and dropped: deferring the screening into the next tile's K-steps, with one
+// pending group or a second accumulator set, cost more in the K-loop than it hid.)
+// =============================================================================================
+template <int DT, int KCAP>
+__global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
+    int n_rows, int n_q, int n_ktiles, int n_row_tiles, uint32_t row_base, int k_out,
+    uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits, int qblocks,
+    int flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1;
+  const int wq = wave & 1;
+  const int fr = lane & 31;
+  const int fh = lane >> 5;
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q0 = qb * kTileQ;
+  const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
+  const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
+
+  uint64_t L[2][KCAP];
+  float thr[2];
+  uint64_t thk[2];
+#pragma unroll
+  for (int bj = 0; bj < 2; ++bj) {
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[bj][j] = 0;
+    const int q = q0 + wq * 64 + bj * 32 + fr;
+    thr[bj] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+    thk[bj] = (q < n_q && thr[bj] != -INFINITY) ? (((uint64_t)ord_f32(thr[bj]) << 32) - 1) : 0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init reads retired before the ring counts
+
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t tile_bytes = (uint32_t)(kTileRows * row_stride);
+  const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, tile_bytes);
+  const bool screen = !(flags & kFlagSkipEpilogue);
+
+  f32x16 acc[2][2];
+  // one k16 step: the wave's 2x2 MFMA blocks
+  auto frag_mma = [&](const u32x4 (&a)[2], const u32x4 (&b)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) mfma_step<DT>(a[bi], b[bj], acc[bi][bj]);
+  };
+  // a tile's first k16 step: accumulate onto 0 (an inline constant, no register zeroing)
+  auto frag_mma_first = [&](const u32x4 (&a)[2], const u32x4 (&b)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        f32x16 z = {};
+        mfma_step<DT>(a[bi], b[bj], z);
+        acc[bi][bj] = z;
+      }
+  };
+
+  // Survivor stash: a passing score's key is appended to a 4-entry register stash of its
+  // column (a few instructions); the sorted list absorbs the stash only when it fills (and at
+  // the end), which is also when the list can raise the column's threshold. Survivors are rare
+  // once the pre-pass seeds the thresholds (~0.4 per lane and column over a whole split on the
+  // C2 data), so the common path never runs the list insert or the k-th select.
+  constexpr int kStash = 4;
+  uint64_t S0[kStash], S1[kStash];
+  int n0 = 0, n1 = 0;
+  auto flush0 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < kStash; ++c)
+      if (c < n0) list_insert<KCAP>(L[0], S0[c]);
+    n0 = 0;
+    const uint64_t kth = list_at<KCAP>(L[0], k_out - 1);
+    if (kth > thk[0]) {
+      thk[0] = kth;
+      thr[0] = key_score(kth);
+    }
+  };
+  auto flush1 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < kStash; ++c)
+      if (c < n1) list_insert<KCAP>(L[1], S1[c]);
+    n1 = 0;
+    const uint64_t kth = list_at<KCAP>(L[1], k_out - 1);
+    if (kth > thk[1]) {
+      thk[1] = kth;
+      thr[1] = key_score(kth);
+    }
+  };
+
+  // ---- tile end: groups (bi, bj) whose max reaches the threshold of column bj; one passing group
+  // per lane per round is staged in the lane's private 64-B LDS slot, and its passing scores go
+  // to the column's stash, one per set bit of a pass mask in a divergent loop.
+  float* slot = reinterpret_cast<float*>(smem + kOffBuf1) + tid * 16;
+  auto screen_tile = [&](int r0) __attribute__((always_inline)) {
+    uint32_t gmask = 0;
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        float m0 = acc[bi][bj][0], m1 = acc[bi][bj][1];
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+          m0 = fmaxf(m0, acc[bi][bj][r]);
+          m1 = fmaxf(m1, acc[bi][bj][r + 1]);
+        }
+        gmask |= (fmaxf(m0, m1) >= thr[bj] ? 1u : 0u) << (bj * 2 + bi);
+      }
+    if (flags & kFlagMaxOnly) {  // ablation: group maxima only (wrong results)
+      if (gmask == 0xFu && thr[0] == 1234.5f) part_keys[0] = 1;
+      return;
+    }
+    while (__ballot(gmask != 0)) {
+      const int sel = gmask ? __builtin_ctz(gmask) : -1;
+      gmask &= gmask - 1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (sel == g) {  // static branch per group, taken only where some lane selected it
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
+            f32x4 v4 = {acc[g & 1][g >> 1][4 * c4], acc[g & 1][g >> 1][4 * c4 + 1], acc[g & 1][g >> 1][4 * c4 + 2],
+                        acc[g & 1][g >> 1][4 * c4 + 3]};
+            *reinterpret_cast<f32x4*>(slot + 4 * c4) = v4;
+          }
+        }
+      }
+      if (sel >= 0) {
+        const int bjs = sel >> 1;
+        const int rb = r0 + wr * 64 + (sel & 1) * 32 + 4 * fh;
+        const float th = bjs ? thr[1] : thr[0];
+        const uint64_t tk = bjs ? thk[1] : thk[0];
+        uint32_t pm = 0;
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * c4 + e;
+            pm |= (v4[e] >= th && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
+          }
+        }
+        while (pm) {
+          const int r = __builtin_ctz(pm);
+          pm &= pm - 1;
+          const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
+          if (key > tk) {
+            if (bjs == 0) {
+#pragma unroll
+              for (int c = 0; c < kStash; ++c)
+                if (n0 == c) S0[c] = key;
+              if (++n0 == kStash) flush0();
+            } else {
+#pragma unroll
+              for (int c = 0; c < kStash; ++c)
+                if (n1 == c) S1[c] = key;
+              if (++n1 == kStash) flush1();
+            }
+          }
+        }
+      }
+    }
+  };
+
+  // Two 128-B k-tile buffers: tile kt+1 streams in (buffer LDS-DMA) while kt is multiplied.
+  // Wave w fills rows [32w, 32w+32) of both tiles, 8 rows (1 KiB) per instruction; lane l lands
+  // at (row 8j + l/8, physical chunk l%8) and loads logical chunk (l%8) ^ swz(row).
+  const int ld_row = lane >> 3;
+  uint32_t ld_off[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave_u * 32 + 8 * j + ld_row;
+    ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+  }
+  for (int t = t_begin; t < t_end; ++t) {
+    const int r0 = t * kTileRows;
+    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)r0 * row_stride, tile_bytes);
+    auto stage = [&](int kt, unsigned char* buf) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = ld_off[j] + kt * kRowBytes;
+        blds16(c_rsrc, off, buf + (wave_u * 32 + 8 * j) * kRowBytes);
+        blds16(q_rsrc, off, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
+      }
+    };
+    const bool load = !(flags & kFlagNoLoads) || t == t_begin;  // ablation: LDS + MFMA ceiling
+    if (load) stage(0, smem + kOffBuf0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();  // also: every wave is past the previous tile's epilogue (slot reuse below)
+    for (int kt = 0; kt < n_ktiles; ++kt) {
+      if (kt + 1 < n_ktiles && load) stage(kt + 1, smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0));
+      const unsigned char* buf = smem + ((kt & 1) ? kOffBuf1 : kOffBuf0);
+      // two fragment register sets, order pinned with sched_barrier: the LDS reads of step g+1
+      // are in flight while the MFMAs of step g run
+      u32x4 fa0[2], fb0[2], fa1[2], fb1[2];
+      auto frag_load = [&](int g, u32x4 (&a)[2], u32x4 (&b)[2]) __attribute__((always_inline)) {
+        const int ch = 2 * g + fh;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+          a[bi] = *reinterpret_cast<const u32x4*>(buf + swz(wr * 64 + bi * 32 + fr, ch));
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+          b[bj] = *reinterpret_cast<const u32x4*>(buf + kTileRows * kRowBytes + swz(wq * 64 + bj * 32 + fr, ch));
+      };
+      frag_load(0, fa0, fb0);
+      frag_load(1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt == 0)
+        frag_mma_first(fa0, fb0);
+      else
+        frag_mma(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_load(2, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_load(3, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_mma(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 landed (this wave's part)
+      lds_barrier();                                    // ... everyone's; everyone done with kt
+    }
+    if (screen) screen_tile(r0);
+  }
+  if (!screen) {  // ablation: GEMM only, keep acc live, no top-k
+    float sink = 0.f;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sink += acc[bi][bj][r];
+    if (sink == 1234.5678f) part_keys[0] = 1;
+    return;
+  }
+
+  if (n0) flush0();
+  if (n1) flush1();
+  // merge the 4 partial lists of each query (2 row-waves x 2 lane halves) through LDS
+  __syncthreads();
+  uint64_t* xl = reinterpret_cast<uint64_t*>(smem);
+  const int part = wr * 2 + fh;
+#pragma unroll
+  for (int bj = 0; bj < 2; ++bj) {
+    const int ql = wq * 64 + bj * 32 + fr;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) xl[(ql * 4 + part) * KCAP + j] = L[bj][j];
+  }
+  __syncthreads();
+  if (tid < kTileQ && q0 + tid < n_q) {
+    uint64_t M[KCAP];
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) M[j] = xl[(tid * 4) * KCAP + j];
+    for (int u = 1; u < 4; ++u) {
+      const uint64_t* src = xl + (tid * 4 + u) * KCAP;
+      for (int j = 0; j < KCAP; ++j) {
+        const uint64_t kk = src[j];
+        if (kk <= M[KCAP - 1]) break;  // sorted: nothing further can enter
+        list_insert<KCAP>(M, kk);
+      }
+    }
+    uint64_t* dst = part_keys + ((int64_t)(q0 + tid) * n_splits + split) * k_out;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j)
+      if (j < k_out) dst[j] = M[j];
+  }
+}
+
 
 // =============================================================================================
 // lane kernel: waves arranged WR (along corpus rows) x WQ (along queries); each wave owns NB
@@ -641,9 +815,7 @@ struct Cfg {
 // 64-B rows: a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the row so the 16
 // rows of a ds_read_b128 lane group ({0-3,12-15,20-27} / {4-11,16-19,28-31}) hit 16 distinct
 // 16-B slots.
-__device__ __forceinline__ int swz(int row, int chunk) {
-  return row * kRowBytes + ((chunk ^ ((row >> 2) & 3)) << 4);
-}
+__device__ __forceinline__ int swz(int row, int chunk) { return swz64(row, chunk); }
 }  // namespace lanek
 
 template <int DT, int KCAP, int NB, int BJ, int WR, int WQ, int STAGES, int MINB>
@@ -1200,8 +1372,9 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
     (void)hipEventRecord(ix->prof_events[(size_t)ix->prof_calls * (kStages + 1) + stage], s);
 }
 
-// ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128
-enum { KERNEL_V1 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2 };
+// ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
+// 3 = 128x128 ping-pong (deferred screening)
+enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3 };
 
 struct SearchPlan {
   int kernel;
@@ -1211,24 +1384,26 @@ struct SearchPlan {
 
 // Corpus and query buffers are padded to whole 256-row tiles (the wide kernel's tile).
 constexpr int64_t kRowPad = 256;
-// The 256x256 lane kernel from this batch on; below it the 128x128 tile kernel (with its
-// lane-local epilogue) is as fast or faster (MI355X, hotpot90k: tile 128 ahead up to 2048,
-// even at 4096, lane 256 ~5 % ahead at 8192).
+// The 256x256 lane kernel from this batch on; below it the 128x128 lane-local tile kernel is as
+// fast or faster (MI355X, hotpot90k).
 constexpr int kWideMinBatch = 6144;
 
 // Resident workgroups of the 128x128 tile kernel: 2 per CU (VGPR/LDS limited).
-constexpr int kResidentSlotsV1 = 256 * 2;
+constexpr int kResidentSlots128 = 256 * 2;
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
-  p.kernel = KERNEL_V1;
+  p.kernel = KERNEL_TILE128;
   if (k <= 16 && !(ix->debug_flags & kFlagTile128)) {
     if (ix->debug_flags & kFlagLane256q128)
       p.kernel = KERNEL_LANE256Q128;
-    else if (B >= kWideMinBatch)
+
+    else if (B >= kWideMinBatch && !(ix->debug_flags & kFlagTileLane))
       p.kernel = KERNEL_LANE256;
+    else
+      p.kernel = KERNEL_TILELANE;
   }
-  if (p.kernel != KERNEL_V1) {
+  if (p.kernel == KERNEL_LANE256 || p.kernel == KERNEL_LANE256Q128) {
     // Row tile TR, query tile TQ, `per_cu` resident workgroups per CU. One wave of workgroups;
     // splits a multiple of 8 (rounded down: an extra workgroup would run as a second wave) so
     // the XCD remap keeps a split's query blocks on one XCD.
@@ -1244,13 +1419,12 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     return p;
   }
-  const int kResidentSlots = kResidentSlotsV1;
   p.qblocks = (int)cdiv(B, kTileQ);
   p.n_row_tiles = (int)cdiv(ix->count, kTileRows);
   // One wave of workgroups: at most the resident slots, splits rounded DOWN to a multiple of 8
   // (an extra workgroup would run as a second wave) so the XCD remap keeps a split's query
   // blocks on one XCD; the kernel balances tile ranges over the splits.
-  int want = std::max(1, kResidentSlots / p.qblocks);
+  int want = std::max(1, kResidentSlots128 / p.qblocks);
   want = std::min(want, std::max(1, p.n_row_tiles));
   p.xcd_remap = want >= 8;
   p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
@@ -1271,7 +1445,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
   }
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
   const int64_t qblocks = cdiv(B, kTileQ);
-  const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlotsV1, qblocks)), 8) * 8;
+  const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlots128, qblocks)), 8) * 8;
   const int64_t wide_splits = std::max<int64_t>(1, 512 / cdiv(B, 128));  // >= any plan's
   const int64_t p_need =
       (int64_t)B * std::max<int64_t>(std::max(max_splits, wide_splits), kSampleMax / kTileRows) * k;
@@ -1329,6 +1503,23 @@ void launch_lane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
 }
 
 // lane lists sized to k: 8, 12 or 16 keys (insert and select cost scale with the size)
+template <int DT, int KCAP>
+void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                     const float* thr, int flags, hipStream_t s) {
+  constexpr int lds = 2 * kBufBytes;  // the staging double buffer (also the end-merge exchange)
+  static_assert(kTileQ * 4 * KCAP * 8 <= lds, "end merge exchange must fit");
+  static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
+  constexpr auto kern = &topk_tilelane_kernel<DT, KCAP>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(kThreads), lds, s, ix->rows, ix->qbuf,
+                     ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes, p.n_row_tiles, row_base, k,
+                     ix->part, thr, p.n_splits, p.qblocks, flags);
+}
+
 template <int DT, int NB, int BJ, int WR, int WQ, int STAGES, int MINB>
 void launch_lane_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                    const float* thr, int flags, hipStream_t s) {
@@ -1361,6 +1552,14 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
   if (p.kernel == KERNEL_LANE256Q128) {
     launch_lane_k<DT, 8, 1, 1, 4, 2, 2>(ix, p, n, B, k, row_base, thr, flags, s);
+    return;
+  }
+  if (p.kernel == KERNEL_TILELANE) {
+    switch (k <= 8 ? 8 : (k <= 12 ? 12 : 16)) {  // lists sized to k
+      case 8: launch_tilelane<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s); break;
+      case 12: launch_tilelane<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s); break;
+      default: launch_tilelane<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s); break;
+    }
     return;
   }
   if (p.kernel == KERNEL_LANE256) {

@@ -216,7 +216,8 @@ def main() -> None:
         elem = 4 if dtype == "f32" else 2
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
         plan = local.plan(B, k)
-        kname = "topk_lane_kernel" if plan["kernel"].startswith("lane") else "topk_tile_kernel"
+        kname = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
+                 "tilelane128": "topk_tilelane_kernel"}.get(plan["kernel"], "topk_tile_kernel")
         out = {
             "metric": METRIC,
             "value": round(value, 1),

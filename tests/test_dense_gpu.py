@@ -203,8 +203,19 @@ def test_lane_f32_bit_exact(cuda, n, d, B, k):
     np.testing.assert_array_equal(s, es.astype(np.float32))
 
 
+def test_default_plans(cuda):
+    from ah_rag.embeddings import DenseIndex
+    ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
+    ix.upsert(np.zeros((90000, 768), np.float32))
+    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
+    assert ix.plan(1, 16)["kernel"] == "tilelane128"
+    assert ix.plan(6144, 10)["kernel"] == "lane256"
+    assert ix.plan(1024, 17)["kernel"] == "tile128"
+    ix.close()
+
+
 @pytest.mark.parametrize("k,sample", [(10, 8192), (16, 8192), (5, 0), (10, 0), (1, 8192)])
-def test_lane_equals_tile128(cuda, k, sample):
+def test_lane_kernels_bitwise_equal(cuda, k, sample):
     """All kernels chain the same 16-deep MFMA steps in k order: bitwise equal results. Sample 0
     (no pre-pass) makes every score of the first tiles a candidate: full scans / overflow rounds."""
     from ah_rag.embeddings import DenseIndex
@@ -216,8 +227,10 @@ def test_lane_equals_tile128(cuda, k, sample):
     ix.set_sample_rows(sample)
     assert ix.plan(len(Q), k)["kernel"] == "lane256"
     a = [t.cpu().numpy() for t in ix.query(Q, k)]
-    # 8: 128x128 tile kernel; 64: lane kernel with 256x128 workgroup tiles
-    for flags, name in ((8, "tile128"), (64, "lane256x128")):
+    # 8: 128x128 tile kernel, cooperative screening; 64: lane kernel with 256x128 workgroup
+    # tiles; 32: 128x128 lane-local tile kernel (the default below B = 6144)
+    variants = [(8, "tile128"), (64, "lane256x128"), (32, "tilelane128")]
+    for flags, name in variants:
         ix.set_debug_flags(flags)
         assert ix.plan(len(Q), k)["kernel"] == name
         b = [t.cpu().numpy() for t in ix.query(Q, k)]
