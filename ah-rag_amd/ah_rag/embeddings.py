@@ -179,6 +179,11 @@ class DenseIndex:
     def truncate(self, count: int = 0) -> None:
         nat.check(nat.lib().ahr_index_truncate(self._h, int(count)), "ahr_index_truncate")
 
+    def set_workspace(self, slot: int) -> None:
+        """Query workspace (0..3) for the following queries: batches in flight on different
+        streams must use different workspaces (include/ahr.h ahr_index_set_workspace)."""
+        nat.check(nat.lib().ahr_index_set_workspace(self._h, int(slot)), "ahr_index_set_workspace")
+
     def reserve(self, max_batch: int, max_k: int = nat.AHR_MAX_K) -> None:
         with torch.cuda.device(self.device):
             nat.check(nat.lib().ahr_index_reserve(self._h, int(max_batch), int(max_k)), "ahr_index_reserve")
@@ -200,7 +205,8 @@ class DenseIndex:
 
     def set_debug_flags(self, flags: int) -> None:
         """Ablation switches (include/ahr.h): 2 = skip the top-k epilogue (garbage results),
-        8 = 128x128 tile kernel, 64 = 256x128 lane kernel, 256 = group maxima only (garbage)."""
+        8 = 128x128 tile kernel (cooperative), 32 = 128x128 lane-local kernel at any batch,
+        64 = 256x128 lane kernel, 256 = group maxima only (garbage)."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
     _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128")

@@ -1321,6 +1321,17 @@ __global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restric
 using namespace ahr;
 using namespace ahr::dense;
 
+// One query workspace: converted queries, per-split partial lists, pre-pass scores/thresholds.
+struct ahr_query_ws {
+  uint8_t* qbuf = nullptr;
+  int64_t q_cap = 0;
+  uint64_t* part = nullptr;
+  int64_t part_cap = 0;
+  float* sample = nullptr;
+  int64_t sample_cap = 0;
+};
+constexpr int kMaxWorkspaces = 4;
+
 struct ahr_index {
   int dim = 0;
   int dtype = 0;
@@ -1339,6 +1350,10 @@ struct ahr_index {
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
   int64_t sample_cap = 0;   // floats
   int sample_rows = 8192;   // S; 0 disables the threshold pre-pass
+  // The fields above (qbuf .. sample_cap) are the ACTIVE query workspace; the others are parked
+  // here (ahr_index_set_workspace swaps them) so batches on different streams never share one.
+  ahr_query_ws parked[kMaxWorkspaces];
+  int cur_ws = 0;
   int debug_flags = 0;      // ablation flags (kFlagSkipEpilogue); 0 in production
   // Optional stage timing: a ring of HIP events, kStages+1 per query call, recorded on the
   // call's stream (ahr_index_profile_begin / _end).
@@ -1432,7 +1447,10 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   return p;
 }
 
-int ensure_query_ws(ahr_index* ix, int B, int k) {
+// Grows the active workspace. A new query buffer is zeroed on the caller's stream: a blocking
+// null-stream memset is not ordered against non-blocking streams and could land after the
+// conversion kernel of the first batch on this workspace.
+int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
   const int64_t q_need = cdiv(B, kRowPad) * kRowPad;
   if (q_need > ix->q_cap) {
     if (ix->qbuf) AHR_HIP(hipFree(ix->qbuf));
@@ -1440,7 +1458,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k) {
     ix->q_cap = 0;
     if (hipMalloc(&ix->qbuf, q_need * ix->row_stride) != hipSuccess)
       return fail(AHR_ENOMEM, "query workspace allocation failed");
-    AHR_HIP(hipMemset(ix->qbuf, 0, q_need * ix->row_stride));
+    AHR_HIP(hipMemsetAsync(ix->qbuf, 0, q_need * ix->row_stride, s));
     ix->q_cap = q_need;
   }
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
@@ -1614,7 +1632,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     return fail(AHR_ERANGE, "row ids must fit in 32 bits");
   DeviceGuard dg(ix->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int st = ensure_query_ws(ix, B, k);
+  int st = ensure_query_ws(ix, B, k, s);
   if (st) return st;
   prof_mark(ix, 0, s);
   hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
@@ -1664,7 +1682,8 @@ int ahr_index_create(int dim, int dtype, int64_t capacity, int device, ahr_index
     delete ix;
     return fail(AHR_ENOMEM, "corpus allocation failed");
   }
-  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess) {
+  // zeroed before any stream (also non-blocking ones) writes rows into it
+  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     (void)hipFree(ix->rows);
     delete ix;
     return fail(AHR_EHIP, "corpus memset failed");
@@ -1680,6 +1699,12 @@ int ahr_index_destroy(ahr_index* ix) {
   if (ix->qbuf) (void)hipFree(ix->qbuf);
   if (ix->part) (void)hipFree(ix->part);
   if (ix->sample) (void)hipFree(ix->sample);
+  for (int w = 0; w < kMaxWorkspaces; ++w) {
+    if (w == ix->cur_ws) continue;
+    if (ix->parked[w].qbuf) (void)hipFree(ix->parked[w].qbuf);
+    if (ix->parked[w].part) (void)hipFree(ix->parked[w].part);
+    if (ix->parked[w].sample) (void)hipFree(ix->parked[w].sample);
+  }
   for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
   delete ix;
   return AHR_OK;
@@ -1815,6 +1840,29 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   return AHR_OK;
 }
 
+int ahr_index_set_workspace(ahr_index* ix, int slot) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (slot < 0 || slot >= kMaxWorkspaces) return fail(AHR_EINVAL, "workspace slot out of range");
+  if (slot == ix->cur_ws) return AHR_OK;
+  ahr_query_ws& out = ix->parked[ix->cur_ws];
+  out.qbuf = ix->qbuf;
+  out.q_cap = ix->q_cap;
+  out.part = ix->part;
+  out.part_cap = ix->part_cap;
+  out.sample = ix->sample;
+  out.sample_cap = ix->sample_cap;
+  ahr_query_ws& in = ix->parked[slot];
+  ix->qbuf = in.qbuf;
+  ix->q_cap = in.q_cap;
+  ix->part = in.part;
+  ix->part_cap = in.part_cap;
+  ix->sample = in.sample;
+  ix->sample_cap = in.sample_cap;
+  in = ahr_query_ws{};
+  ix->cur_ws = slot;
+  return AHR_OK;
+}
+
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks) {
   if (!ix || B <= 0 || k <= 0 || k > AHR_MAX_K) return fail(AHR_EINVAL, "bad plan request");
@@ -1830,7 +1878,10 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   if (max_batch <= 0 || max_k <= 0 || max_k > AHR_MAX_K) return fail(AHR_EINVAL, "bad reserve sizes");
   DeviceGuard dg(ix->device);
-  return ensure_query_ws(ix, max_batch, max_k);
+  const int st = ensure_query_ws(ix, max_batch, max_k, nullptr);
+  if (st) return st;
+  AHR_HIP(hipDeviceSynchronize());  // zeroing done before any stream uses the workspace
+  return AHR_OK;
 }
 
 int ahr_index_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, float* scores,

@@ -55,6 +55,8 @@ def parse_args():
                     help="nccl = RCCL (default); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight (one stream + index workspace each); rows-sharded runs use 1")
     ap.add_argument("--recall-queries", type=int, default=256)
     return ap.parse_args()
 
@@ -146,44 +148,68 @@ def main() -> None:
     salt = rank if args.shard == "queries" else 0
     q, src = corpus.queries(B, rows, salt=salt)
     index.reserve(B, k)
-    scores = torch.empty((B, k), dtype=torch.float32, device=dev)
-    out_rows = torch.empty((B, k), dtype=torch.int32, device=dev)
     keys = torch.empty((B, k), dtype=torch.int64, device=dev)
+    # Batches in flight: batch i runs on stream i % inflight with index workspace i % inflight,
+    # so the latency-bound stages of one batch (query conversion, pre-pass k-th selection, merge,
+    # launch gaps) overlap the neighbouring batch's tile kernel. Every batch still runs the whole
+    # path; only the order of independent batches' kernels on the GPU changes.
+    inflight = 1 if sharded else max(1, args.inflight)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(inflight - 1)]
+    outs = [(torch.empty((B, k), dtype=torch.float32, device=dev), torch.empty((B, k), dtype=torch.int32, device=dev))
+            for _ in range(inflight)]
+    for i in range(inflight):
+        local.set_workspace(i)
+        local.reserve(B, k)
+    local.set_workspace(0)
+    for st in streams[1:]:
+        st.wait_stream(streams[0])  # queries and index are ready
+    counter = [0]
 
-    def step():
+    def step(depth: int):
         if sharded:
             index.query_keys(q, k, out=keys)
             gathered = all_gather_keys(keys)                  # RCCL all-gather over xGMI
             s_, r_, _ = merge_topk_keys(gathered.permute(1, 0, 2).contiguous(), k)
             return s_, r_
-        local.query(q, k, out=(scores, out_rows))
-        return scores, out_rows
+        i = counter[0] % depth
+        counter[0] += 1
+        local.set_workspace(i)
+        return local.query(q, k, stream=streams[i], out=outs[i])
 
-    for _ in range(args.warmup):
-        step()
+    def timed(depth: int) -> float:
+        for _ in range(args.warmup):
+            step(depth)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(depth)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    dt_serial = timed(1) if inflight > 1 else None
+    counter[0] = 0
+    dt = timed(inflight)
+    local.set_workspace(0)
+    res = step(1)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
     # Stage timings (HIP events between the kernels of a step) in a separate, untimed pass: the
     # event records themselves add ~6 us of GPU-side gap per stage boundary.
     local.profile_begin(args.steps)
     for _ in range(args.steps):
-        step()
+        step(1)
     torch.cuda.synchronize()
     prof = local.profile_end()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, dt_serial or 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = float(t[0].item())
+        dt_serial = float(t[1].item()) if dt_serial is not None else None
 
     q_per_step = B * world if not sharded else B
     value = q_per_step * args.steps / dt
@@ -238,6 +264,8 @@ def main() -> None:
                 "corpus_rows": N, "dim": d, "batch": B, "top_k": k, "index_dtype": dtype,
                 "parallelism": (f"rows{world}" if sharded else (f"queries{world}" if world > 1 else "single")),
                 "launch": plan,
+                "inflight": inflight,
+                "serial_ms_per_step": round(dt_serial / args.steps * 1e3, 4) if dt_serial else None,
             },
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
             "roofline": {

@@ -116,6 +116,13 @@ int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits
 /* Pre-size the per-query workspace so ahr_index_query() allocates nothing (graph-capturable). */
 int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k);
 
+/* Select the query workspace (0..3; default 0) that the following ahr_index_query /
+ * ahr_index_query_keys / ahr_index_reserve calls use: the converted queries, per-split partial
+ * lists and pre-pass buffers. Calls on different workspaces may run concurrently on different
+ * streams (a serving loop keeping several batches in flight); calls on one workspace must be
+ * ordered on one stream. No reference counterpart (the reference is one synchronous call). */
+int ahr_index_set_workspace(ahr_index* ix, int slot);
+
 /* Replaces coll.query(query_embeddings=[q], n_results=k) (hierarchical_graph.py:714), batched.
  * q: device fp32 [B][dim]; scores: device fp32 [B][k] (descending); rows: device int32 [B][k].
  * Ties order by row ascending. If fewer than k live rows exist the tail is (-inf, -1).

@@ -253,3 +253,30 @@ def test_lane_ties_order_by_row(cuda):
     es, er = dr.topk(C, Q, 16, mode="fma")
     np.testing.assert_array_equal(r, er)
     np.testing.assert_array_equal(s, es.astype(np.float32))
+
+
+def test_workspaces_concurrent_streams(cuda):
+    """Batches in flight on two streams with two query workspaces == the same batches run one by
+    one (workspaces share nothing but the read-only corpus)."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(14)
+    C = _clustered(rng, 40000, 768)
+    Qs = [torch.from_numpy(_clustered(rng, B, 768)).to(cuda) for B in (1024, 700, 1024, 300)]
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    serial = [[t.cpu().numpy() for t in ix.query(q, 10)] for q in Qs]
+    streams = [torch.cuda.current_stream(cuda), torch.cuda.Stream(device=cuda)]
+    streams[1].wait_stream(streams[0])
+    outs = []
+    for rep in range(3):
+        for i, q in enumerate(Qs):
+            ix.set_workspace(i % 2)
+            outs.append(ix.query(q, 10, stream=streams[i % 2]))
+    torch.cuda.synchronize()
+    ix.set_workspace(0)
+    for j, (s, r) in enumerate(outs):
+        np.testing.assert_array_equal(r.cpu().numpy(), serial[j % len(Qs)][1])
+        np.testing.assert_array_equal(s.cpu().numpy(), serial[j % len(Qs)][0])
+    with pytest.raises(Exception):
+        ix.set_workspace(4)
+    ix.close()
