@@ -184,6 +184,7 @@ enum {
   kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
   kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
   kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
+  kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
 };
 constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
@@ -729,8 +730,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
       __builtin_amdgcn_sched_barrier(0);
       frag_mma(fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 landed (this wave's part)
-      lds_barrier();                                    // ... everyone's; everyone done with kt
+      if (!(flags & kFlagNoWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 landed
+      lds_barrier();  // ... everyone's; everyone done with kt
     }
     if (screen) screen_tile(r0);
   }
@@ -1836,7 +1837,7 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kKernelFlags);
+  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kKernelFlags);
   return AHR_OK;
 }
 
