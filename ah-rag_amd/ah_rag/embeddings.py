@@ -206,10 +206,11 @@ class DenseIndex:
     def set_debug_flags(self, flags: int) -> None:
         """Ablation switches (include/ahr.h): 2 = skip the top-k epilogue (garbage results),
         8 = 128x128 tile kernel (cooperative), 32 = 128x128 lane-local kernel at any batch,
-        64 = 256x128 lane kernel, 256 = group maxima only (garbage)."""
+        64 = 256x128 lane kernel, 256 = group maxima only (garbage), 2048 = plan without the
+        query-resident kernel, 4096 = the query-resident kernel wherever it applies."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
-    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128")
+    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

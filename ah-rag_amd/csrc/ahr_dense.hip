@@ -185,8 +185,10 @@ enum {
   kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
   kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
   kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
+  kFlagNoQres = 2048,     // plan without the query-resident kernel
+  kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
 };
-constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128;
+constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
@@ -779,6 +781,317 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
   }
 }
 
+// =============================================================================================
+// topk_qkv_kernel (default for bf16/f16 with d_pad = 64 * NKT, k <= 16): the query-resident
+// scheme at two waves per SIMD. A workgroup of 8 waves owns 128 queries (one workgroup per CU);
+// waves w and w + 4 hold the same 32 queries but opposite halves of the dimension, so each keeps
+// only half of the B fragments in registers (96 VGPRs at d = 768). A ring slot ("phase") holds
+// k-step j of the tile for the first half and k-step j + NKT/2 for the second. At a tile's end
+// the two partial accumulators of a pair meet through LDS (each wave sends the two 32-row blocks
+// the other one screens; partial(half 0) + partial(half 1)), and each wave screens its two
+// blocks: 16-row group maxima against the query's threshold, passing groups to the candidate
+// buffer (a list in private memory takes over when it is full). After the K-loop each lane folds
+// its candidate groups (read back from its own buffer, L2-resident) into a register top-k list,
+// so the sorted inserts never stall the MFMA pipe; the lists of (query, split, half) go to the
+// lane-list merge. Per corpus byte brought in from L2: 128 queries x 2 flops (the two-operand
+// 128 x 128 tile kernels: 64). (Measured and dropped: all 32 queries' fragments in registers at
+// one wave per SIMD — LDS latency, DMA issue and the screening were exposed.)
+// =============================================================================================
+namespace qkv {
+constexpr int kTR = 128;
+constexpr int kHalfBytes = kTR * kRowBytes;         // one 64-deep k-step of 128 rows: 16 KiB
+constexpr int kSlotBytes = 2 * kHalfBytes;          // a phase: the k-steps of both halves
+constexpr int kXBytes = 4 * 2 * 2 * 4 * 64 * 16;    // exchange [group][from half][block][c4][lane] x 16 B
+template <int ST>
+struct Cfg {
+  static constexpr int kOffX = ST * kSlotBytes;
+  static constexpr int kLds = kOffX + kXBytes;
+  static_assert(kLds <= 160 * 1024, "qkv LDS exceeds 160 KiB");
+};
+}  // namespace qkv
+
+template <int DT, int NKT, int ST, int KCAP>
+__global__ __launch_bounds__(512, 1) void topk_qkv_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
+    int n_rows, int n_q, int n_row_tiles, uint32_t row_base, int k_out,
+    uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits, int qblocks,
+    int flags, uint64_t* __restrict__ cand_keys, int cand_cap) {
+  static_assert(DT != DT_F32, "fp32 keeps the two-operand tile kernels (exact fma-chain contract)");
+  constexpr int NH = NKT / 2;  // k-steps per half
+  static_assert(NKT % 2 == 0 && NH % ST == 0 && ST >= 3, "ring slots must divide the phases of a tile");
+  using C = qkv::Cfg<ST>;
+  constexpr int TR = qkv::kTR;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int qg = wave & 3;
+  const int kh = wave >> 2;
+  const int fr = lane & 31;
+  const int fh = lane >> 5;
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q = qb * kTileQ + qg * 32 + fr;
+  const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
+  const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
+
+  // B fragments of this lane's query over this wave's half: k16 group i of the half covers
+  // elements kh * 64 NH + [16i, 16i + 16); lane half fh holds 8 of them.
+  u32x4 Bq[4 * NH];
+  {
+    const uint8_t* qrow = queries + (int64_t)q * row_stride + kh * NH * kRowBytes + fh * 16;
+#pragma unroll
+    for (int i = 0; i < 4 * NH; ++i) Bq[i] = *reinterpret_cast<const u32x4*>(qrow + i * 32);
+  }
+  float thr = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+  uint64_t thk = (q < n_q && thr != -INFINITY) ? (((uint64_t)ord_f32(thr) << 32) - 1) : 0;
+  // Fallback list (sorted, descending): private memory, touched only when the lane's candidate
+  // buffer is full, so it costs no registers in the K-loop.
+  volatile uint64_t Ls[KCAP];  // volatile: kept in scratch, not promoted to registers
+#pragma unroll 1
+  for (int j = 0; j < KCAP; ++j) Ls[j] = 0;
+  // candidate key buffer of producer (query q, split, half kh, lane half fh)
+  const int64_t cbase = ((int64_t)q * (4 * n_splits) + 4 * split + 2 * kh + fh) * cand_cap;
+  int nc = 0;
+
+  if (t_begin < t_end) {
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t tile_bytes = (uint32_t)(TR * row_stride);
+    // DMA fill: wave w fills half w / 4, rows [32 (w % 4), +32) of a phase slot, 8 rows per
+    // instruction; lane l lands at (row 8j + l/8, physical chunk l%8), logical chunk (l%8) ^ swz.
+    // rows 8j and 8j + 16 share the swizzle: two lane offsets, the +16 rows via soffset
+    uint32_t ld_off[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (wave_u & 3) * 32 + 8 * j + (lane >> 3);
+      ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+    }
+    const uint32_t off16 = (uint32_t)(16 * row_stride);
+    auto issue = [&](int tile, int ph, int slot) __attribute__((always_inline)) {
+      tile = tile < t_end ? tile : t_end - 1;  // past the split: a harmless refill of a dead slot
+      const __amdgpu_buffer_rsrc_t r = tile_rsrc(corpus + (int64_t)tile * TR * row_stride, tile_bytes);
+      unsigned char* dst = smem + slot * qkv::kSlotBytes + (wave_u >> 2) * qkv::kHalfBytes + (wave_u & 3) * 32 * kRowBytes;
+      const int kstep = (wave_u >> 2) * NH + ph;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + j * 8 * kRowBytes),
+                                                 16, ld_off[j & 1], kstep * kRowBytes + (j >> 1) * off16, 0, 0);
+    };
+    uint32_t fo[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) fo[g] = (uint32_t)(kh * qkv::kHalfBytes + swz(fr, 2 * g + fh));
+    auto frag_read = [&](int slot, int g, u32x4 (&F)[4]) __attribute__((always_inline)) {
+      const unsigned char* base = smem + slot * qkv::kSlotBytes + fo[g];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) F[b] = *reinterpret_cast<const u32x4*>(base + b * 32 * kRowBytes);
+    };
+
+    f32x16 acc[4];
+    // One fragment set: block b's fragment of the next k16 group is read right after block b's
+    // MFMA of this group has issued, 4 MFMAs (128 cycles) before it is used (16 VGPRs, not 32).
+    u32x4 F[4];
+    auto mma_read = [&](int bi, bool first, int rslot, int rg) __attribute__((always_inline)) {
+      const unsigned char* base = smem + rslot * qkv::kSlotBytes + fo[rg];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (first) {
+          f32x16 z = {};
+          mfma_step<DT>(F[b], Bq[bi], z);
+          acc[b] = z;
+        } else {
+          mfma_step<DT>(F[b], Bq[bi], acc[b]);
+        }
+        F[b] = *reinterpret_cast<const u32x4*>(base + b * 32 * kRowBytes);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+
+    // exchange regions: this wave writes X[qg][kh] and reads X[qg][1 - kh]; the one it read is
+    // then its private 64-B-per-lane staging slot for the list fallback
+    f32x4* xw = reinterpret_cast<f32x4*>(smem + C::kOffX + (qg * 2 + kh) * 8192) + lane;
+    const f32x4* xr = reinterpret_cast<const f32x4*>(smem + C::kOffX + (qg * 2 + (1 - kh)) * 8192) + lane;
+    float* slot = reinterpret_cast<float*>(smem + C::kOffX + (qg * 2 + (1 - kh)) * 8192) + lane * 16;
+
+    auto screen_blocks = [&](int r0, int b0) __attribute__((always_inline)) {
+      // b0: first of the two blocks this wave screens (compile-time at each call site)
+      uint32_t gmask = 0;
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        const int b = b0 + bb;
+        float m0 = acc[b][0], m1 = acc[b][1];
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+          m0 = fmaxf(m0, acc[b][r]);
+          m1 = fmaxf(m1, acc[b][r + 1]);
+        }
+        gmask |= (fmaxf(m0, m1) >= thr ? 1u : 0u) << b;
+      }
+      if (flags & kFlagMaxOnly) {  // ablation: group maxima only (wrong results)
+        if (gmask == 0xFu && thr == 1234.5f) part_keys[0] = 1;
+        return;
+      }
+      while (__ballot(gmask != 0)) {
+        const int sel = gmask ? __builtin_ctz(gmask) : -1;
+        gmask &= gmask - 1;
+        // the group's 16 scores go through the lane's 64-B LDS slot; each score that beats the
+        // admission key is appended to the lane's candidate key buffer (one 8-B store), or, once
+        // that is full, inserted into the private fallback list (which raises the threshold)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int b = b0 + bb;
+          if (sel == b) {
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4)
+              *reinterpret_cast<f32x4*>(slot + 4 * c4) =
+                  f32x4{acc[b][4 * c4], acc[b][4 * c4 + 1], acc[b][4 * c4 + 2], acc[b][4 * c4 + 3]};
+          }
+        }
+        if (sel >= 0) {
+          const int rb = r0 + sel * 32 + 4 * fh;
+          uint32_t pm = 0;
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
+            const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * c4 + e;
+              pm |= (v4[e] >= thr && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
+            }
+          }
+          while (pm) {
+            const int r = __builtin_ctz(pm);
+            pm &= pm - 1;
+            const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + (r & 3) + 8 * (r >> 2)));
+            if (key > thk) {
+              if (nc < cand_cap) {
+                cand_keys[cbase + nc] = key;
+                ++nc;
+              } else {  // thk >= the list's k-th >= its last: key enters, the last drops
+                int j = KCAP - 1;
+#pragma unroll 1
+                while (j > 0 && Ls[j - 1] < key) {
+                  Ls[j] = Ls[j - 1];
+                  --j;
+                }
+                Ls[j] = key;
+                const uint64_t kth = Ls[k_out - 1];
+                if (kth > thk) {
+                  thk = kth;
+                  thr = key_score(kth);
+                }
+              }
+            }
+          }
+        }
+      }
+    };
+    auto tile_end = [&](int r0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (kh == h) {  // wave-uniform; compile-time block indices inside
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            const int b = (h == 0 ? 2 : 0) + bb;  // the partner's blocks
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4)
+              xw[(bb * 4 + c4) * 64] = f32x4{acc[b][4 * c4], acc[b][4 * c4 + 1], acc[b][4 * c4 + 2], acc[b][4 * c4 + 3]};
+          }
+        }
+      }
+      lds_barrier();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (kh == h) {
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            const int b = (h == 0 ? 0 : 2) + bb;  // own blocks: partial(half 0) + partial(half 1)
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+              const f32x4 v = xr[(bb * 4 + c4) * 64];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[b][4 * c4 + e] = acc[b][4 * c4 + e] + v[e];
+            }
+          }
+          if (!(flags & kFlagSkipEpilogue)) screen_blocks(r0, h == 0 ? 0 : 2);
+        }
+      }
+    };
+
+    // Ring of ST phase slots. Before phase j's data is used, barrier B(j): this wave's DMA of phase
+    // j landed (vmcnt leaves the ST-2 younger phases in flight), lgkmcnt(0) (every wave's reads
+    // of phase j-1 are done), s_barrier; then phase j+ST-1 is issued into slot (j-1) % ST. B(j+1)
+    // sits inside phase j, after its last fragment reads, so phase j+1's first reads overlap
+    // phase j's last MFMAs.
+    constexpr int kVm = 4 * (ST - 2);
+#pragma unroll
+    for (int c = 0; c < ST - 1; ++c) issue(t_begin, c, c);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVm) : "memory");
+    lds_barrier();
+    issue(t_begin, ST - 1, ST - 1);
+    frag_read(0, 0, F);
+    for (int t = t_begin; t < t_end; ++t) {
+#pragma unroll
+      for (int ph = 0; ph < NH; ++ph) {
+        const int sl = ph % ST;
+        __builtin_amdgcn_sched_barrier(0);
+        mma_read(4 * ph + 0, ph == 0, sl, 1);
+        mma_read(4 * ph + 1, false, sl, 2);
+        mma_read(4 * ph + 2, false, sl, 3);
+        if (!(flags & kFlagNoWait)) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVm) : "memory");
+          lds_barrier();
+        }
+        if (!(flags & kFlagNoLoads)) issue(t + (ph + ST) / NH, (ph + ST) % NH, sl);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_read(4 * ph + 3, false, (ph + 1) % ST, 0);
+      }
+      tile_end(t * TR);
+    }
+    if (flags & kFlagSkipEpilogue) {
+      float sink = 0.f;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sink += acc[b][r];
+      if (sink == 1234.5678f) part_keys[0] = 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
+  }
+
+  // Fold the candidate keys into a register list (candidate rows and the fallback list's rows are
+  // disjoint), merge lanes l and l ^ 32 (disjoint rows of one query) and write one list per
+  // (query, split, half).
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = Ls[j];
+  for (int g0 = 0; g0 < nc; g0 += 8) {  // 8 loads in flight, then the inserts
+    uint64_t c8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c8[u] = g0 + u < nc ? cand_keys[cbase + g0 + u] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (c8[u]) list_insert<KCAP>(L, c8[u]);
+  }
+  uint64_t P[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) P[j] = shfl_xor_u64(L[j], 32);
+  if (fh == 0 && q < n_q) {
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) list_insert<KCAP>(L, P[j]);
+    uint64_t* dst = part_keys + ((int64_t)q * (2 * n_splits) + 2 * split + kh) * k_out;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j)
+      if (j < k_out) dst[j] = L[j];
+  }
+}
 
 // =============================================================================================
 // lane kernel: waves arranged WR (along corpus rows) x WQ (along queries); each wave owns NB
@@ -1330,6 +1643,8 @@ struct ahr_query_ws {
   int64_t part_cap = 0;
   float* sample = nullptr;
   int64_t sample_cap = 0;
+  uint8_t* cand = nullptr;
+  int64_t cand_cap = 0;
 };
 constexpr int kMaxWorkspaces = 4;
 
@@ -1350,8 +1665,10 @@ struct ahr_index {
   int64_t part_cap = 0;  // uint64 elements
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
   int64_t sample_cap = 0;   // floats
+  uint8_t* cand = nullptr;  // query-resident kernel: candidate groups (counts, row bases, scores)
+  int64_t cand_cap = 0;     // bytes
   int sample_rows = 8192;   // S; 0 disables the threshold pre-pass
-  // The fields above (qbuf .. sample_cap) are the ACTIVE query workspace; the others are parked
+  // The fields above (qbuf .. cand_cap) are the ACTIVE query workspace; the others are parked
   // here (ahr_index_set_workspace swaps them) so batches on different streams never share one.
   ahr_query_ws parked[kMaxWorkspaces];
   int cur_ws = 0;
@@ -1389,8 +1706,9 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 }
 
 // ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
-// 3 = 128x128 ping-pong (deferred screening)
-enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3 };
+// 3 = 128x128 lane-local tile kernel, 5 = query-resident kernel (dimension halves over wave pairs);
+// 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed)
+enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5 };
 
 struct SearchPlan {
   int kernel;
@@ -1407,9 +1725,35 @@ constexpr int kWideMinBatch = 6144;
 // Resident workgroups of the 128x128 tile kernel: 2 per CU (VGPR/LDS limited).
 constexpr int kResidentSlots128 = 256 * 2;
 
+// The query-resident kernel keeps a 128-query block's fragments in registers: bf16/f16 and the
+// dimensions it is instantiated for (d_pad = 384, 768). Its admission threshold is the pre-pass
+// seed (raised only by the fallback list), so it is planned where the seed samples at least 1/32
+// of the corpus, and from B = 2048 on, where it measured ahead of the lane-local tile kernel
+// (hotpot90k: 276 vs 282 us at B = 2048, 531 vs 581 us at 4096; behind at 1024, 153 vs 147, and
+// at 5M rows, 11.2 vs 9.1 ms). Debug flag kFlagQkv plans it at any size.
+bool qkv_ok(const ahr_index* ix, int B, int k) {
+  const int nkt = ix->d_pad * ix->elem / kRowBytes;
+  if (k > 16 || ix->dtype == AHR_F32 || !(nkt == 6 || nkt == 12)) return false;
+  if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres)) return false;
+  if (ix->debug_flags & kFlagQkv) return true;
+  return B >= 2048 && ix->sample_rows > 0 && ix->count <= 32 * (int64_t)ix->sample_rows;
+}
+
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
+  if (qkv_ok(ix, B, k)) {
+    // one workgroup per CU (512 VGPRs per lane): one wave of 256 workgroups
+    p.kernel = KERNEL_QKV;
+    p.qblocks = (int)cdiv(B, kTileQ);
+    p.n_row_tiles = (int)cdiv(ix->count, qkv::kTR);
+    int want = std::max(1, 256 / p.qblocks);
+    want = std::min(want, std::max(1, p.n_row_tiles));
+    p.xcd_remap = want >= 8;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    return p;
+  }
   if (k <= 16 && !(ix->debug_flags & kFlagTile128)) {
     if (ix->debug_flags & kFlagLane256q128)
       p.kernel = KERNEL_LANE256Q128;
@@ -1539,6 +1883,49 @@ void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B
                      ix->part, thr, p.n_splits, p.qblocks, flags);
 }
 
+// Candidate keys per producer (query, split, half, lane half): one per tile of the split covers
+// the C2 survivor rate (~1 row per producer) many times over; a full buffer falls back to the
+// lane's private list inside the kernel, so the cap only trades memory for speed.
+inline int qkv_cand_cap(const SearchPlan& p) { return (int)std::min(64, std::max(16, p.tiles_per_split)); }
+inline int64_t cand_bytes(int B, const SearchPlan& p) { return (int64_t)B * 4 * p.n_splits * qkv_cand_cap(p) * 8; }
+
+int ensure_cand(ahr_index* ix, int64_t bytes) {
+  if (bytes <= ix->cand_cap) return AHR_OK;
+  if (ix->cand) AHR_HIP(hipFree(ix->cand));
+  ix->cand = nullptr;
+  ix->cand_cap = 0;
+  if (hipMalloc(&ix->cand, bytes) != hipSuccess) return fail(AHR_ENOMEM, "candidate workspace allocation failed");
+  ix->cand_cap = bytes;
+  return AHR_OK;
+}
+
+template <int DT, int NKT, int ST, int KCAP>
+void launch_qkv(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                const float* thr, int flags, hipStream_t s) {
+  constexpr int lds = qkv::Cfg<ST>::kLds;
+  constexpr auto kern = &topk_qkv_kernel<DT, NKT, ST, KCAP>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), lds, s, ix->rows, ix->qbuf,
+                     ix->row_stride, n_rows, B, p.n_row_tiles, row_base, k, ix->part, thr, p.n_splits, p.qblocks,
+                     flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
+}
+
+template <int DT, int NKT>
+void launch_qkv_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                  const float* thr, int flags, hipStream_t s) {
+  constexpr int ST = 3;  // phase slots of 32 KiB (+ 64 KiB exchange) in 160 KiB
+  if (k <= 8)
+    launch_qkv<DT, NKT, ST, 8>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  else if (k <= 12)
+    launch_qkv<DT, NKT, ST, 12>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+  else
+    launch_qkv<DT, NKT, ST, 16>(ix, p, n_rows, B, k, row_base, thr, flags, s);
+}
+
 template <int DT, int NB, int BJ, int WR, int WQ, int STAGES, int MINB>
 void launch_lane_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                    const float* thr, int flags, hipStream_t s) {
@@ -1569,6 +1956,15 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
+  if constexpr (DT != DT_F32) {
+    if (p.kernel == KERNEL_QKV) {
+      if (ix->d_pad * ix->elem / kRowBytes == 12)
+        launch_qkv_k<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s);
+      else
+        launch_qkv_k<DT, 6>(ix, p, n, B, k, row_base, thr, flags, s);
+      return;
+    }
+  }
   if (p.kernel == KERNEL_LANE256Q128) {
     launch_lane_k<DT, 8, 1, 1, 4, 2, 2>(ix, p, n, B, k, row_base, thr, flags, s);
     return;
@@ -1640,6 +2036,10 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
                      (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                      ix->row_stride, ix->d_pad, ix->dtype);
   SearchPlan p = plan_search(ix, B, k);
+  if (p.kernel == KERNEL_QKV && ix->count > 0) {
+    st = ensure_cand(ix, cand_bytes(B, p));
+    if (st) return st;
+  }
   if (ix->count > 0) {
     switch (ix->dtype) {
       case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, s); break;
@@ -1651,7 +2051,10 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     prof_mark(ix, 2, s);
   }
   prof_mark(ix, 3, s);
-  launch_merge(ix->part, B, ix->count > 0 ? p.n_splits : 0, k, k, scores, rows, keys, s);
+  {
+    const int lists = (p.kernel == KERNEL_QKV ? 2 : 1) * p.n_splits;  // qkv: one list per (split, half)
+    launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
+  }
   prof_mark(ix, 4, s);
   if (ix->prof_calls < ix->prof_max_calls) ++ix->prof_calls;
   AHR_HIP(hipGetLastError());
@@ -1700,11 +2103,13 @@ int ahr_index_destroy(ahr_index* ix) {
   if (ix->qbuf) (void)hipFree(ix->qbuf);
   if (ix->part) (void)hipFree(ix->part);
   if (ix->sample) (void)hipFree(ix->sample);
+  if (ix->cand) (void)hipFree(ix->cand);
   for (int w = 0; w < kMaxWorkspaces; ++w) {
     if (w == ix->cur_ws) continue;
     if (ix->parked[w].qbuf) (void)hipFree(ix->parked[w].qbuf);
     if (ix->parked[w].part) (void)hipFree(ix->parked[w].part);
     if (ix->parked[w].sample) (void)hipFree(ix->parked[w].sample);
+    if (ix->parked[w].cand) (void)hipFree(ix->parked[w].cand);
   }
   for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
   delete ix;
@@ -1852,6 +2257,8 @@ int ahr_index_set_workspace(ahr_index* ix, int slot) {
   out.part_cap = ix->part_cap;
   out.sample = ix->sample;
   out.sample_cap = ix->sample_cap;
+  out.cand = ix->cand;
+  out.cand_cap = ix->cand_cap;
   ahr_query_ws& in = ix->parked[slot];
   ix->qbuf = in.qbuf;
   ix->q_cap = in.q_cap;
@@ -1859,6 +2266,8 @@ int ahr_index_set_workspace(ahr_index* ix, int slot) {
   ix->part_cap = in.part_cap;
   ix->sample = in.sample;
   ix->sample_cap = in.sample_cap;
+  ix->cand = in.cand;
+  ix->cand_cap = in.cand_cap;
   in = ahr_query_ws{};
   ix->cur_ws = slot;
   return AHR_OK;
@@ -1879,8 +2288,16 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   if (max_batch <= 0 || max_k <= 0 || max_k > AHR_MAX_K) return fail(AHR_EINVAL, "bad reserve sizes");
   DeviceGuard dg(ix->device);
-  const int st = ensure_query_ws(ix, max_batch, max_k, nullptr);
+  int st = ensure_query_ws(ix, max_batch, max_k, nullptr);
   if (st) return st;
+  // candidate groups of the query-resident plan at the current corpus size
+  for (int kk = 1; kk <= max_k; kk = kk < 8 ? 8 : kk + 8) {
+    const SearchPlan p = plan_search(ix, max_batch, kk);
+    if (p.kernel == KERNEL_QKV) {
+      st = ensure_cand(ix, cand_bytes(max_batch, p));
+      if (st) return st;
+    }
+  }
   AHR_HIP(hipDeviceSynchronize());  // zeroing done before any stream uses the workspace
   return AHR_OK;
 }

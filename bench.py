@@ -58,6 +58,8 @@ def parse_args():
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (one stream + index workspace each); rows-sharded runs use 1")
     ap.add_argument("--recall-queries", type=int, default=256)
+    ap.add_argument("--debug-flags", type=int, default=0,
+                    help="ablation/kernel-selection switches (DenseIndex.set_debug_flags); 0 in production")
     return ap.parse_args()
 
 
@@ -145,6 +147,8 @@ def main() -> None:
         index = local = DenseIndex(d, N, dtype=dtype, device=dev)
         for s0 in range(0, N, 1_000_000):
             local.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
+    if args.debug_flags:
+        local.set_debug_flags(args.debug_flags)
     salt = rank if args.shard == "queries" else 0
     q, src = corpus.queries(B, rows, salt=salt)
     index.reserve(B, k)
@@ -243,7 +247,8 @@ def main() -> None:
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
         plan = local.plan(B, k)
         kname = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
-                 "tilelane128": "topk_tilelane_kernel"}.get(plan["kernel"], "topk_tile_kernel")
+                 "tilelane128": "topk_tilelane_kernel",
+                 "qkv128": "topk_qkv_kernel"}.get(plan["kernel"], "topk_tile_kernel")
         out = {
             "metric": METRIC,
             "value": round(value, 1),

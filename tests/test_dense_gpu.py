@@ -209,8 +209,21 @@ def test_default_plans(cuda):
     ix.upsert(np.zeros((90000, 768), np.float32))
     assert ix.plan(1024, 10)["kernel"] == "tilelane128"
     assert ix.plan(1, 16)["kernel"] == "tilelane128"
-    assert ix.plan(6144, 10)["kernel"] == "lane256"
+    assert ix.plan(2048, 10)["kernel"] == "qkv128"
+    assert ix.plan(6144, 10)["kernel"] == "qkv128"
     assert ix.plan(1024, 17)["kernel"] == "tile128"
+    ix.set_debug_flags(4096)
+    assert ix.plan(1024, 10)["kernel"] == "qkv128"
+    ix.set_debug_flags(2048)  # without the query-resident kernel
+    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
+    assert ix.plan(6144, 10)["kernel"] == "lane256"
+    ix.close()
+    ix = DenseIndex(768, 400000, dtype="f16", device=cuda)  # seed samples < 1/32 of the rows
+    ix.upsert(np.zeros((300000, 768), np.float32))
+    assert ix.plan(4096, 10)["kernel"] == "tilelane128"
+    ix.close()
+    ix = DenseIndex(1024, 1000, dtype="bf16", device=cuda)  # not a query-resident dimension
+    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
     ix.close()
 
 
@@ -225,11 +238,15 @@ def test_lane_kernels_bitwise_equal(cuda, k, sample):
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     ix.set_sample_rows(sample)
-    assert ix.plan(len(Q), k)["kernel"] == "lane256"
+    ix.set_debug_flags(4096)
+    assert ix.plan(len(Q), k)["kernel"] == "qkv128"
+    d = [t.cpu().numpy() for t in ix.query(Q, k)]  # default: half-dimension partials, own rounding
+    ix.set_debug_flags(32)
     a = [t.cpu().numpy() for t in ix.query(Q, k)]
+    _close_topk(d, a)
     # 8: 128x128 tile kernel, cooperative screening; 64: lane kernel with 256x128 workgroup
-    # tiles; 32: 128x128 lane-local tile kernel (the default below B = 6144)
-    variants = [(8, "tile128"), (64, "lane256x128"), (32, "tilelane128")]
+    # tiles; 32: 128x128 lane-local tile kernel; 2048: previous default (256x256 lane kernel)
+    variants = [(8, "tile128"), (64, "lane256x128"), (32, "tilelane128"), (2048, "lane256")]
     for flags, name in variants:
         ix.set_debug_flags(flags)
         assert ix.plan(len(Q), k)["kernel"] == name
@@ -280,3 +297,66 @@ def test_workspaces_concurrent_streams(cuda):
     with pytest.raises(Exception):
         ix.set_workspace(4)
     ix.close()
+
+
+# ---- query-resident kernel (bf16/f16, d_pad 384/768, k <= 16) ----------------------------------
+
+def _close_topk(a, b, tol=2e-6):
+    """Two kernels' (scores, rows): scores within tol; a row differs only where another of the
+    returned scores lies within tol of it (a near-tie reordered or swapped at the k-th place)."""
+    np.testing.assert_allclose(a[0], b[0], rtol=0, atol=tol)
+    mism = a[1] != b[1]
+    if mism.any():
+        gap = np.abs(a[0][:, :, None] - b[0][:, None, :])
+        near = (gap < tol).sum(axis=2) >= 2  # a tie group inside the list (order swapped)
+        near[:, -1] = True                   # or the k-th place (a tie with a row outside)
+        assert near[mism].all()
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n,d,B,k,sample", [
+    (40001, 768, 1024, 10, 8192), (40001, 768, 1024, 10, 0), (33000, 384, 300, 16, 8192),
+    (300, 768, 1, 1, 0), (1000, 384, 129, 8, 0), (90000, 768, 2048, 5, 8192),
+    (5000, 768, 7000, 12, 0)])
+def test_qkv_matches_tilelane(cuda, dtype, n, d, B, k, sample):
+    """The query-resident kernel sums two half-dimension partials (each a k-ordered chain of the
+    same 16-deep MFMA steps): scores within 2e-6 of the lane-local tile kernel, the same rows
+    except exact-score near-ties; with and without the threshold pre-pass, for splits with no
+    tiles (n = 300: 3 tiles over 3 splits), ragged query blocks and k."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(77 + n + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    ix.set_sample_rows(sample)
+    ix.set_debug_flags(4096)
+    assert ix.plan(B, k)["kernel"] == "qkv128"
+    a = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(32)
+    assert ix.plan(B, k)["kernel"] == "tilelane128"
+    b = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.close()
+    _close_topk(a, b)
+    # and against the f64 oracle on the rounded inputs (sampled queries)
+    sel = np.arange(0, B, max(1, B // 64))
+    Cr = dr.round_to_storage(C, dtype)
+    es, _ = dr.topk(Cr, dr.round_to_storage(Q[sel], dtype), k, mode="f64")
+    assert np.abs(a[0][sel, :min(k, n)] - es[:, :min(k, n)]).max() < 1e-4
+
+
+def test_qkv_ties_order_by_row(cuda):
+    """bf16 duplicate rows score identically: the lowest row ids win, across tiles and splits."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(13)
+    base = _clustered(rng, 300, 768)
+    C = np.concatenate([base] * 40)  # 12000 rows, each vector 40 times
+    pick = rng.integers(0, 300, 600)
+    Q = base[pick]
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ix.set_debug_flags(4096)
+    assert ix.plan(len(Q), 16)["kernel"] == "qkv128"
+    s, r = [t.cpu().numpy() for t in ix.query(Q, 16)]
+    ix.close()
+    np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(16)[None, :])
+    assert (s == s[:, :1]).all()
