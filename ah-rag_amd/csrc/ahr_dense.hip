@@ -1446,12 +1446,17 @@ __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict_
   const int q = blockIdx.x;
   const int lane = threadIdx.x;
   const float* src = scores + (int64_t)q * S;
-  uint32_t v[kGroupMax / 64];
+  // all loads in flight at once (clamped addresses, masked after): a per-lane guard around each
+  // load serialised them, one memory latency per 64 values
+  float raw[kGroupMax / 64];
 #pragma unroll
   for (int j = 0; j < kGroupMax / 64; ++j) {
     const int i = lane + 64 * j;
-    v[j] = i < S ? ord_f32(src[i]) : 0u;
+    raw[j] = 64 * j < S ? src[i < S ? i : S - 1] : 0.f;  // 64 j < S is wave-uniform
   }
+  uint32_t v[kGroupMax / 64];
+#pragma unroll
+  for (int j = 0; j < kGroupMax / 64; ++j) v[j] = lane + 64 * j < S ? ord_f32(raw[j]) : 0u;
   // 20 bits from the MSB (sign, exponent, 11 mantissa bits): ans is the largest 20-bit prefix
   // with #{v >= ans} >= k, so ans <= the k-th largest value: a valid, ~5e-4-relative bound.
   uint32_t ans = 0;
@@ -1561,6 +1566,53 @@ __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restri
   if (i >= n) return;
   const float* x = src + i * dim;
   const bool vec = (dim & 3) == 0;
+  if (vec && d_pad <= 1024 && dt != DT_F32) {
+    // Fast path (bf16/f16 rows up to 1024 wide): the whole row in flight at once (clamped
+    // addresses, masked after); the general loop below waits on each 1-KiB piece in turn. Same
+    // arithmetic and order as the loop: the per-lane fma chain in j order, then the butterfly.
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 4 * lane + 256 * u;
+      v[u] = *reinterpret_cast<const f32x4*>(x + (j < dim ? j : dim - 4));
+      if (j >= dim) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float nrm = 1.f;
+    if (normalize) {
+      float s = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s = fmaf(v[u][0], v[u][0], s); s = fmaf(v[u][1], v[u][1], s);
+        s = fmaf(v[u][2], v[u][2], s); s = fmaf(v[u][3], v[u][3], s);
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+      nrm = fmaxf(sqrtf(s), 1e-12f);
+    }
+    const int64_t slot = slots ? slots[i] : start + i;
+    uint8_t* row = dst + slot * row_stride;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 4 * lane + 256 * u;
+      if (j >= d_pad) break;
+      f32x4 w4 = v[u];
+      if (normalize) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w4[e] = w4[e] / nrm;
+      }
+      if (dt == DT_BF16) {
+        uint2 w;
+        w.x = (uint32_t)f32_to_bf16_rne(w4[0]) | ((uint32_t)f32_to_bf16_rne(w4[1]) << 16);
+        w.y = (uint32_t)f32_to_bf16_rne(w4[2]) | ((uint32_t)f32_to_bf16_rne(w4[3]) << 16);
+        *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
+      } else {
+        _Float16* o = reinterpret_cast<_Float16*>(row) + j;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (_Float16)w4[e];
+      }
+    }
+    return;
+  }
   float nrm = 1.f;
   if (normalize) {
     float s = 0.f;
