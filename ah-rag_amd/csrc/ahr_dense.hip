@@ -1782,13 +1782,18 @@ constexpr int kResidentSlots128 = 256 * 2;
 // seed (raised only by the fallback list), so it is planned where the seed samples at least 1/32
 // of the corpus, and from B = 2048 on, where it measured ahead of the lane-local tile kernel
 // (hotpot90k: 276 vs 282 us at B = 2048, 531 vs 581 us at 4096; behind at 1024, 153 vs 147, and
-// at 5M rows, 11.2 vs 9.1 ms). Debug flag kFlagQkv plans it at any size.
+// at 5M rows, 11.2 vs 9.1 ms; a seed from 1/350 of random data: 1.5 ms vs 0.39 ms — a full
+// candidate buffer's fallback list lives in private memory, and folding the buffer into it to
+// raise the threshold made the normal case slower, 591 vs 531 us at 4096). Debug flag kFlagQkv
+// plans it at any size.
 bool qkv_ok(const ahr_index* ix, int B, int k) {
   const int nkt = ix->d_pad * ix->elem / kRowBytes;
   if (k > 16 || ix->dtype == AHR_F32 || !(nkt == 6 || nkt == 12)) return false;
   if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres)) return false;
   if (ix->debug_flags & kFlagQkv) return true;
-  return B >= 2048 && ix->sample_rows > 0 && ix->count <= 32 * (int64_t)ix->sample_rows;
+  // B <= 8192: at least 4 splits, so a producer's share of the survivors (~10 x N / S per query
+  // on random-order data) fits its candidate buffer
+  return B >= 2048 && B <= 8192 && ix->sample_rows > 0 && ix->count <= 32 * (int64_t)ix->sample_rows;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
