@@ -41,7 +41,8 @@ NODE_TYPE_CODES = {"entity": NODE_ENTITY, "summary": NODE_SUMMARY, "hyperedge": 
 NODE_TYPE_NAMES = {NODE_ENTITY: "entity", NODE_SUMMARY: "summary", NODE_HYPEREDGE: "hyperedge",
                    NODE_OTHER: None}
 
-AHR_MAX_K = 32
+AHR_MAX_K = 32          # fused kernels (and ahr_topk_merge)
+AHR_MAX_K_LARGE = 4096  # ahr_index_query / _query_keys (scores + radix select beyond AHR_MAX_K)
 AHR_ADJ_COUNT = 6
 
 # Every symbol include/ahr.h declares (tests check the library exports all of them).

@@ -478,8 +478,8 @@ class HierarchicalGraph:
                      return_cluster: bool = False, db_path: Optional[str] = None,
                      model_name: Optional[str] = None, query_vectors: Optional[np.ndarray] = None) -> List[Any]:
         """search() over many queries with one device pass (B = len(queries))."""
-        if top_k > nat.AHR_MAX_K:
-            raise ValueError(f"top_k={top_k} exceeds the fused kernel's limit ({nat.AHR_MAX_K})")
+        if top_k > nat.AHR_MAX_K_LARGE:
+            raise ValueError(f"top_k={top_k} exceeds the dense index limit ({nat.AHR_MAX_K_LARGE})")
         params = resolve_search_params(self.G.graph.get("search_params", {}), top_k, member_top_m, alpha, beta,
                                        gamma, delta, judge_overall_min, confidence_min, type_filter)
         vi = self.G.graph.get("vector_index") if isinstance(self.G.graph.get("vector_index"), dict) else {}

@@ -265,7 +265,7 @@ class SearchEngine:
             stream: Optional[torch.cuda.Stream] = None) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
         """Dense top_k -> expansion -> rerank for a batch. Returns host (rows, scores, result)."""
         k = max(1, params.top_k)
-        k_dense = min(k, nat.AHR_MAX_K)
+        k_dense = min(k, nat.AHR_MAX_K_LARGE)
         scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
         valid = rows >= 0
         nodes = torch.where(valid, self.row_to_node[rows.clamp_min(0).long()], torch.full_like(rows, -1))

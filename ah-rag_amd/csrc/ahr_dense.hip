@@ -175,7 +175,7 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) 
   return v;
 }
 
-enum { MODE_TOPK = 0, MODE_GROUPMAX = 1 };
+enum { MODE_TOPK = 0, MODE_GROUPMAX = 1, MODE_SCORES = 2 };
 enum {
   kFlagXcdRemap = 1,
   kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
@@ -195,6 +195,8 @@ constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | k
 //             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
 //             valid lower bound of its final k-th best (from the sampled pre-pass).
 // MODE_GROUPMAX: 16-row group maxima of the scores into score_out [n_q][score_ld] (pre-pass).
+// MODE_SCORES  : every score into score_out [n_q][score_ld], row-indexed (top-k beyond the
+//                register lists, k > AHR_MAX_K: radix_topk_kernel selects from them).
 template <int DT, int KCAP, int MODE>
 __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride,
@@ -327,6 +329,26 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tile_kernel(
       lds_barrier();                                    // ... everyone's; everyone done with kt
     }
 
+    if constexpr (MODE == MODE_SCORES) {
+      // lane: query column fr of block bj, rows 4 fh + (r & 3) + 8 (r >> 2) of block bi
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        const int q = q0 + wq * 64 + bj * 32 + fr;
+        if (q >= n_q) continue;
+        float* dst = score_out + (int64_t)q * score_ld;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          const int rb = r0 + wr * 64 + bi * 32 + 4 * fh;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rb + (r & 3) + 8 * (r >> 2);
+            if (row < n_rows) dst[row] = acc[bi][bj][r];
+          }
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     if constexpr (MODE == MODE_GROUPMAX) {
       // Threshold pre-pass: per query, the max of each 16-row group (one lane's 16 registers of
       // one 32x32 block). The k-th largest group max is a valid lower bound of the k-th best
@@ -1544,6 +1566,113 @@ __global__ __launch_bounds__(64) void merge_heads_kernel(const uint64_t* __restr
   }
 }
 
+// Exact top-k for k beyond the register lists (AHR_MAX_K < k <= AHR_MAX_K_LARGE) from a score
+// row [n] of one query (MODE_SCORES output): one workgroup per query. (1) The k-th largest
+// ordered score T by 4 passes of 8-bit radix histograms in LDS, MSB first. (2) One pass in row
+// order keeps every score above T and, of those equal to T, the lowest rows (a block-wide
+// ordered count), as packed keys. (3) Bitonic sort of the k keys in LDS (score desc, row asc).
+constexpr int kLargeK = 4096;
+
+__global__ __launch_bounds__(256) void radix_topk_kernel(const float* __restrict__ scores, int64_t ld, int n,
+                                                         int k, uint32_t row_base, float* __restrict__ out_s,
+                                                         int32_t* __restrict__ out_r,
+                                                         uint64_t* __restrict__ out_keys, int64_t out_q0) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sel[kLargeK];
+  __shared__ int sh_b, sh_k, sh_eq_seen, sh_n;
+  __shared__ int wsum[4];
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const float* src = scores + (int64_t)q * ld;
+  const int kk0 = k < n ? k : n;
+  uint32_t prefix = 0, mask = 0;
+  int kk = kk0;  // rank still to be found inside the current prefix bucket (1-based)
+  for (int pass = 0; pass < 4 && kk0 > 0; ++pass) {
+    const int shift = 24 - 8 * pass;
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const uint32_t u = ord_f32(src[i]);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int cum = 0, b = 255;
+      for (; b > 0; --b) {
+        if (cum + (int)hist[b] >= kk) break;
+        cum += (int)hist[b];
+      }
+      sh_b = b;
+      sh_k = kk - cum;
+    }
+    __syncthreads();
+    prefix |= (uint32_t)sh_b << shift;
+    mask |= 255u << shift;
+    kk = sh_k;
+    __syncthreads();
+  }
+  // (2) prefix = T (the k-th largest ordered score); kk = how many entries equal to T to keep
+  if (tid == 0) {
+    sh_eq_seen = 0;
+    sh_n = 0;
+  }
+  __syncthreads();
+  for (int base = 0; base < n && kk0 > 0; base += 256) {
+    const int i = base + tid;
+    uint32_t u = 0;
+    float v = 0.f;
+    if (i < n) {
+      v = src[i];
+      u = ord_f32(v);
+    }
+    const bool eq = i < n && u == prefix;
+    // ordered rank of this equal entry among this chunk's equal entries
+    const uint64_t bal = __ballot(eq);
+    const int wrank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+    if (lane == 0) wsum[wave] = __popcll(bal);
+    __syncthreads();
+    int before = sh_eq_seen;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    const bool take = (i < n && u > prefix) || (eq && before + wrank < kk);
+    if (take) {
+      const int pos = atomicAdd(&sh_n, 1);
+      sel[pos] = make_key(v, row_base + (uint32_t)i);
+    }
+    __syncthreads();
+    if (tid == 0) sh_eq_seen += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  // (3) bitonic sort, descending, over the next power of two (zero keys pad at the end)
+  int np2 = 1;
+  while (np2 < kk0) np2 <<= 1;
+  for (int i = kk0 + tid; i < np2; i += 256) sel[i] = 0;
+  __syncthreads();
+  for (int size = 2; size <= np2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < np2; i += 256) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint64_t a = sel[i], b = sel[j];
+          const bool desc = (i & size) == 0;
+          if (desc ? a < b : a > b) {
+            sel[i] = b;
+            sel[j] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < k; j += 256) {
+    const uint64_t key = j < kk0 ? sel[j] : 0;
+    const int64_t o = (out_q0 + q) * k + j;
+    if (out_s) out_s[o] = key ? key_score(key) : -INFINITY;
+    if (out_r) out_r[o] = key ? (int32_t)key_row(key) : -1;
+    if (out_keys) out_keys[o] = key;
+  }
+}
+
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float v) {
   uint32_t u = __float_as_uint(v);
   u += 0x7FFFu + ((u >> 16) & 1u);
@@ -2075,11 +2204,53 @@ void launch_merge(const uint64_t* in, int B, int n_lists, int k_in, int k, float
   }
 }
 
+// k > AHR_MAX_K: every score of a chunk of queries (the 128x128 tile kernel in MODE_SCORES, into
+// the candidate workspace), then radix_topk_kernel per query. Chunks bound the score buffer to
+// 1 GiB.
+template <int DT>
+int run_query_large_k(ahr_index* ix, int B, int k, uint32_t row_base, float* scores, int32_t* rows,
+                      uint64_t* keys, hipStream_t s) {
+  const int64_t n = ix->count;
+  const int64_t ld = cdiv(std::max<int64_t>(n, 1), 64) * 64;
+  int64_t chunk = std::max<int64_t>(kTileQ, ((int64_t)1 << 28) / ld / kTileQ * kTileQ);
+  chunk = std::min<int64_t>(chunk, cdiv(B, kTileQ) * kTileQ);
+  int st = ensure_cand(ix, chunk * ld * (int64_t)sizeof(float));
+  if (st) return st;
+  float* sc = reinterpret_cast<float*>(ix->cand);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tile_kernel<DT, 8, MODE_SCORES>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    attr_set = true;
+  }
+  const int n_row_tiles = (int)cdiv(n, kTileRows);
+  prof_mark(ix, 1, s);
+  prof_mark(ix, 2, s);
+  for (int64_t c0 = 0; c0 < B; c0 += chunk) {
+    const int nq = (int)std::min<int64_t>(chunk, B - c0);
+    const int qblocks = (int)cdiv(nq, kTileQ);
+    const int n_splits = std::max(1, std::min(n_row_tiles, kResidentSlots128 / qblocks));
+    if (n > 0) {
+      hipLaunchKernelGGL((topk_tile_kernel<DT, 8, MODE_SCORES>), dim3((unsigned)(n_splits * qblocks)), dim3(kThreads),
+                         kLdsBytes, s, ix->rows, ix->qbuf + c0 * ix->row_stride, ix->row_stride, (int)n, nq,
+                         ix->d_pad * ix->elem / kRowBytes, 1, n_row_tiles, row_base, k, (uint64_t*)nullptr,
+                         (const float*)nullptr, sc, ld, n_splits, qblocks, 0);
+    }
+    hipLaunchKernelGGL(radix_topk_kernel, dim3((unsigned)nq), dim3(256), 0, s, sc, ld, (int)n, k, row_base, scores,
+                       rows, keys, c0);
+  }
+  prof_mark(ix, 3, s);
+  prof_mark(ix, 4, s);
+  if (ix->prof_calls < ix->prof_max_calls) ++ix->prof_calls;
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
 int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int64_t row_base,
               float* scores, int32_t* rows, uint64_t* keys, void* stream) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   if (B < 0 || k <= 0) return fail(AHR_EINVAL, "B must be >= 0 and k > 0");
-  if (k > AHR_MAX_K) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K (32)");
+  if (k > AHR_MAX_K_LARGE) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K_LARGE (4096)");
   if (B == 0) return AHR_OK;
   if (!q) return fail(AHR_EINVAL, "null query pointer");
   if (row_base < 0 || row_base + ix->count > 0xFFFFFFFFll)
@@ -2092,6 +2263,13 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
                      (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                      ix->row_stride, ix->d_pad, ix->dtype);
+  if (k > AHR_MAX_K) {
+    switch (ix->dtype) {
+      case AHR_BF16: return run_query_large_k<DT_BF16>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);
+      case AHR_F16: return run_query_large_k<DT_F16>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);
+      default: return run_query_large_k<DT_F32>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);
+    }
+  }
   SearchPlan p = plan_search(ix, B, k);
   if (p.kernel == KERNEL_QKV && ix->count > 0) {
     st = ensure_cand(ix, cand_bytes(B, p));

@@ -51,8 +51,11 @@ enum ahr_dtype {
   AHR_BF16 = 2
 };
 
-/* Largest k the fused kernel serves (Chroma n_results). */
+/* Largest k the fused kernels serve (Chroma n_results); ahr_index_query / _query_keys accept k up
+ * to AHR_MAX_K_LARGE through a two-step path (every score of a chunk of queries, then an exact
+ * radix select + bitonic sort per query, same tie rule). ahr_topk_merge: k <= AHR_MAX_K. */
 #define AHR_MAX_K 32
+#define AHR_MAX_K_LARGE 4096
 
 int ahr_abi_version(void);
 const char* ahr_last_error(void);

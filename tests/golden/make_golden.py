@@ -240,6 +240,7 @@ def main() -> None:
             {"top_k": 7, "alpha": 0.5, "beta": 0.3, "gamma": 0.15, "delta": 0.05},
             {"top_k": 4, "member_top_m": 8},
             {"top_k": 12, "type_filter": ["entity", "summary"], "judge_overall_min": 4.0},
+            {"top_k": 40, "member_top_m": 5},  # beyond the fused kernels' 32: the large-k path
         ]
         search_cases = []
         for q in queries:

@@ -360,3 +360,47 @@ def test_qkv_ties_order_by_row(cuda):
     ix.close()
     np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(16)[None, :])
     assert (s == s[:, :1]).all()
+
+
+# ---- k beyond the register lists (AHR_MAX_K < k <= AHR_MAX_K_LARGE): scores + radix select ----
+
+@pytest.mark.parametrize("dtype,n,d,B,k", [
+    ("f32", 5000, 384, 7, 100), ("f32", 3000, 768, 130, 500), ("f32", 700, 256, 3, 1000),
+    ("f32", 50, 128, 2, 40), ("bf16", 20000, 768, 33, 64), ("f16", 9000, 384, 5, 4096)])
+def test_large_k(cuda, dtype, n, d, B, k):
+    """k > 32 (Chroma's n_results has no small cap): fp32 rows and scores bit-identical to the
+    oracle's fma chain; bf16/f16 scores within 1e-4 of the f64 oracle on the rounded inputs,
+    rows equal except near-ties; k > n pads with (-inf, -1)."""
+    rng = np.random.default_rng(4000 + n + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    if dtype != "f32":
+        C, Q = dr.round_to_storage(C, dtype), dr.round_to_storage(Q, dtype)
+    s, r = _run(dtype, C, Q, k, cuda)
+    kk = min(k, n)
+    if dtype == "f32":
+        es, er = dr.topk(C, Q, k, mode="fma")
+        np.testing.assert_array_equal(r[:, :kk], er[:, :kk])
+        np.testing.assert_array_equal(s[:, :kk].astype(np.float32), es[:, :kk].astype(np.float32))
+    else:
+        es, er = dr.topk(C, Q, k, mode="f64")
+        assert np.abs(s[:, :kk] - es[:, :kk]).max() < 1e-4
+        mism = r[:, :kk] != er[:, :kk]
+        if mism.any():
+            full = dr.scores_matrix(C, Q, mode="f64").astype(np.float64)
+            got = np.take_along_axis(full, r[:, :kk], axis=1)
+            assert (np.abs(got[mism] - es[:, :kk][mism]) < 2e-5).all()
+    if kk < k:
+        assert (r[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
+
+
+def test_large_k_ties_order_by_row(cuda):
+    """Duplicate rows tie exactly at and across the radix-select boundary: lowest rows first."""
+    rng = np.random.default_rng(15)
+    base = _clustered(rng, 300, 256)
+    C = np.concatenate([base] * 40)  # 12000 rows, each vector 40 times
+    Q = base[rng.integers(0, 300, 40)]
+    s, r = _run("f32", C, Q, 100, cuda)
+    es, er = dr.topk(C, Q, 100, mode="fma")
+    np.testing.assert_array_equal(r, er)
+    np.testing.assert_array_equal(s, es.astype(np.float32))
