@@ -1673,6 +1673,89 @@ __global__ __launch_bounds__(256) void radix_topk_kernel(const float* __restrict
   }
 }
 
+// Top-k of packed keys (cross-shard merge for k > AHR_MAX_K): keys are unique (row ids differ),
+// so the k-th largest key by 8 passes of 8-bit radix histograms is an exact cut; every key at or
+// above it is kept, then bitonic-sorted in LDS. keys_in [B][n] (0 = empty slot).
+__global__ __launch_bounds__(256) void radix_topk_keys_kernel(const uint64_t* __restrict__ keys_in, int n, int k,
+                                                              float* __restrict__ out_s,
+                                                              int32_t* __restrict__ out_r,
+                                                              uint64_t* __restrict__ out_keys) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sel[kLargeK];
+  __shared__ int sh_b, sh_k, sh_n, sh_live;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint64_t* src = keys_in + (int64_t)q * n;
+  if (tid == 0) {
+    sh_live = 0;
+    sh_n = 0;
+  }
+  __syncthreads();
+  int live = 0;
+  for (int i = tid; i < n; i += 256) live += src[i] != 0;
+  atomicAdd(&sh_live, live);
+  __syncthreads();
+  const int kk0 = k < sh_live ? k : sh_live;
+  uint64_t prefix = 0, mask = 0;
+  int kk = kk0;
+  for (int pass = 0; pass < 8 && kk0 > 0; ++pass) {
+    const int shift = 56 - 8 * pass;
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const uint64_t u = src[i];
+      if (u && (u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int cum = 0, b = 255;
+      for (; b > 0; --b) {
+        if (cum + (int)hist[b] >= kk) break;
+        cum += (int)hist[b];
+      }
+      sh_b = b;
+      sh_k = kk - cum;
+    }
+    __syncthreads();
+    prefix |= (uint64_t)sh_b << shift;
+    mask |= (uint64_t)255 << shift;
+    kk = sh_k;
+    __syncthreads();
+  }
+  for (int i = tid; i < n && kk0 > 0; i += 256) {
+    const uint64_t u = src[i];
+    if (u && u >= prefix) sel[atomicAdd(&sh_n, 1)] = u;
+  }
+  int np2 = 1;
+  while (np2 < kk0) np2 <<= 1;
+  __syncthreads();
+  for (int i = kk0 + tid; i < np2; i += 256) sel[i] = 0;
+  __syncthreads();
+  for (int size = 2; size <= np2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < np2; i += 256) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint64_t a = sel[i], b = sel[j];
+          const bool desc = (i & size) == 0;
+          if (desc ? a < b : a > b) {
+            sel[i] = b;
+            sel[j] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < k; j += 256) {
+    const uint64_t key = j < kk0 ? sel[j] : 0;
+    const int64_t o = (int64_t)q * k + j;
+    if (out_s) out_s[o] = key ? key_score(key) : -INFINITY;
+    if (out_r) out_r[o] = key ? (int32_t)key_row(key) : -1;
+    if (out_keys) out_keys[o] = key;
+  }
+}
+
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float v) {
   uint32_t u = __float_as_uint(v);
   u += 0x7FFFu + ((u >> 16) & 1u);
@@ -2552,10 +2635,14 @@ int ahr_index_query_keys(ahr_index* ix, const float* q, int B, int k, int normal
 int ahr_topk_merge(const uint64_t* keys_in, int B, int n_lists, int k_in, int k, float* scores,
                    int32_t* rows, uint64_t* keys_out, void* stream) {
   if (B < 0 || n_lists < 0 || k_in < 0 || k <= 0) return fail(AHR_EINVAL, "bad merge shape");
-  if (k > AHR_MAX_K) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K (32)");
+  if (k > AHR_MAX_K_LARGE) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K_LARGE (4096)");
   if (B == 0) return AHR_OK;
   if (!keys_in && n_lists * k_in > 0) return fail(AHR_EINVAL, "null keys");
-  launch_merge(keys_in, B, n_lists, k_in, k, scores, rows, keys_out, reinterpret_cast<hipStream_t>(stream));
+  if (k > AHR_MAX_K || k_in > AHR_MAX_K)
+    hipLaunchKernelGGL(radix_topk_keys_kernel, dim3((unsigned)B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       keys_in, n_lists * k_in, k, scores, rows, keys_out);
+  else
+    launch_merge(keys_in, B, n_lists, k_in, k, scores, rows, keys_out, reinterpret_cast<hipStream_t>(stream));
   AHR_HIP(hipGetLastError());
   return AHR_OK;
 }

@@ -53,7 +53,8 @@ enum ahr_dtype {
 
 /* Largest k the fused kernels serve (Chroma n_results); ahr_index_query / _query_keys accept k up
  * to AHR_MAX_K_LARGE through a two-step path (every score of a chunk of queries, then an exact
- * radix select + bitonic sort per query, same tie rule). ahr_topk_merge: k <= AHR_MAX_K. */
+ * radix select + bitonic sort per query, same tie rule); ahr_topk_merge likewise (k or k_in
+ * above AHR_MAX_K: a radix select over the packed keys). */
 #define AHR_MAX_K 32
 #define AHR_MAX_K_LARGE 4096
 

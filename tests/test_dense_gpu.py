@@ -134,24 +134,26 @@ def test_empty_index(cuda):
     ix.close()
 
 
-def test_merge_matches_single_shard(cuda):
-    """Row-sharded search + key merge == unsharded search (the multi-GPU contract, on 1 GPU)."""
+@pytest.mark.parametrize("k", [10, 100])
+def test_merge_matches_single_shard(cuda, k):
+    """Row-sharded search + key merge == unsharded search (the multi-GPU contract, on 1 GPU);
+    k = 100 goes through the large-k query path and the radix key merge."""
     from ah_rag.embeddings import DenseIndex, merge_topk_keys
     rng = np.random.default_rng(8)
     C = _clustered(rng, 30000, 768)
     Q = _clustered(rng, 40, 768)
-    full_s, full_r = _run("f32", C, Q, 10, cuda)
+    full_s, full_r = _run("f32", C, Q, k, cuda)
     for G in (2, 3, 8):
         bounds = np.linspace(0, len(C), G + 1).astype(int)
         lists = []
         for g in range(G):
             ix = DenseIndex(768, bounds[g + 1] - bounds[g], dtype="f32", device=cuda)
             ix.upsert(C[bounds[g]:bounds[g + 1]])
-            lists.append(ix.query_keys(Q, 10, row_base=int(bounds[g])))
+            lists.append(ix.query_keys(Q, k, row_base=int(bounds[g])))
             torch.cuda.synchronize()
             ix.close()
         keys = torch.stack(lists, dim=1)  # [B, G, k]
-        s, r, _ = merge_topk_keys(keys, 10)
+        s, r, _ = merge_topk_keys(keys, k)
         np.testing.assert_array_equal(r.cpu().numpy(), full_r)
         np.testing.assert_array_equal(s.cpu().numpy(), full_s)
 
