@@ -187,6 +187,7 @@ enum {
   kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
   kFlagNoQres = 2048,     // plan without the query-resident kernel
   kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
+  kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
 };
 constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
@@ -706,23 +707,29 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
     const int row = wave_u * 32 + 8 * j + ld_row;
     ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
   }
+  auto stage_t = [&](int t, int kt, unsigned char* buf) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)t * kTileRows * row_stride, tile_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t off = ld_off[j] + kt * kRowBytes;
+      blds16(c_rsrc, off, buf + (wave_u * 32 + 8 * j) * kRowBytes);
+      blds16(q_rsrc, off, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
+    }
+  };
+  // k-tile 0 of the first tile; every later tile's k-tile 0 streams in under the previous tile's
+  // last k-tile and epilogue (into buffer 0, which the last k-tile does not use when n_ktiles is
+  // even), so no tile start waits a full DMA latency
+  const bool even_k = (n_ktiles & 1) == 0 && !(flags & kFlagNoTilePrefetch);
+  stage_t(t_begin, 0, smem + kOffBuf0);
   for (int t = t_begin; t < t_end; ++t) {
     const int r0 = t * kTileRows;
-    const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)r0 * row_stride, tile_bytes);
-    auto stage = [&](int kt, unsigned char* buf) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t off = ld_off[j] + kt * kRowBytes;
-        blds16(c_rsrc, off, buf + (wave_u * 32 + 8 * j) * kRowBytes);
-        blds16(q_rsrc, off, buf + kTileRows * kRowBytes + (wave_u * 32 + 8 * j) * kRowBytes);
-      }
-    };
     const bool load = !(flags & kFlagNoLoads) || t == t_begin;  // ablation: LDS + MFMA ceiling
-    if (load) stage(0, smem + kOffBuf0);
+    if (!even_k && t > t_begin && load) stage_t(t, 0, smem + kOffBuf0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();  // also: every wave is past the previous tile's epilogue (slot reuse below)
     for (int kt = 0; kt < n_ktiles; ++kt) {
-      if (kt + 1 < n_ktiles && load) stage(kt + 1, smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0));
+      if (kt + 1 < n_ktiles && load) stage_t(t, kt + 1, smem + (((kt + 1) & 1) ? kOffBuf1 : kOffBuf0));
+      if (kt + 1 == n_ktiles && even_k && t + 1 < t_end && !(flags & kFlagNoLoads)) stage_t(t + 1, 0, smem + kOffBuf0);
       const unsigned char* buf = smem + ((kt & 1) ? kOffBuf1 : kOffBuf0);
       // two fragment register sets, order pinned with sched_barrier: the LDS reads of step g+1
       // are in flight while the MFMAs of step g run
@@ -754,7 +761,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
       __builtin_amdgcn_sched_barrier(0);
       frag_mma(fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      if (!(flags & kFlagNoWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 landed
+      // stage kt+1 landed (the last k-tile waits for nothing: the next tile's k-tile 0 may still
+      // be in flight, the tile start waits for it after the epilogue)
+      if (!(flags & kFlagNoWait) && kt + 1 < n_ktiles) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();  // ... everyone's; everyone done with kt
     }
     if (screen) screen_tile(r0);
@@ -2560,7 +2569,8 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kKernelFlags);
+  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
+                             kKernelFlags);
   return AHR_OK;
 }
 
