@@ -27,11 +27,13 @@ def node_row(n: Dict[str, Any]) -> List[float]:
 def featurize_observation(obs: Dict[str, Any], k_nodes: int = 10) -> Tuple[np.ndarray, Dict[str, Any]]:
     state = obs.get("state") or {}
     sel = (obs.get("selection") or [])[:k_nodes]
-    vec = np.zeros(4 + NODE_FEATS * k_nodes, np.float32)
-    vec[:4] = [_num(obs.get("step")), len(state.get("selection_ids") or []),
-               len(state.get("frontier_ids") or []), len(obs.get("seeds") or [])]
-    if sel:
-        vec[4:4 + NODE_FEATS * len(sel)] = np.asarray([node_row(n) for n in sel], np.float64).ravel()
+    # one Python list, one float32 conversion (each value rounded once from double, as before)
+    row = [_num(obs.get("step")), float(len(state.get("selection_ids") or [])),
+           float(len(state.get("frontier_ids") or [])), float(len(obs.get("seeds") or []))]
+    for n in sel:
+        row.extend(node_row(n))
+    row.extend([0.0] * (NODE_FEATS * (k_nodes - len(sel))))
+    vec = np.array(row, np.float32)
     return vec, {"top_node_ids": [str(n.get("node_id")) for n in sel]}
 
 

@@ -497,35 +497,39 @@ class HierarchicalGraph:
 
     def _assemble(self, engine: SearchEngine, rows, scores, res, b: int, top_k: int, return_cluster: bool):
         seeds = []
-        for r, s in zip(rows, scores):
+        for r, s in zip(rows.tolist(), scores.tolist()):
             if r < 0:
                 continue
             dist = 1.0 - float(s)  # Chroma's cosine distance of the hit
             seeds.append({"node_id": engine.row_ids[r], "semantic": 1.0 - float(dist), "meta": engine.row_metas[r]})
         n_nodes = engine.graph.n_nodes
+        nodes = self.G.nodes
         reranked = []
-        for j in range(int(res.out_count[b]) if top_k > 0 else 0):
-            idx = int(res.out_nodes[b, j])
+        m = int(res.out_count[b]) if top_k > 0 else 0
+        # one list conversion per array row (numpy scalar indexing per element is the slow part)
+        out_nodes, out_sem, out_score = res.out_nodes[b, :m].tolist(), res.out_sem[b, :m].tolist(), \
+            res.out_score[b, :m].tolist()
+        for idx, sem, score in zip(out_nodes, out_sem, out_score):
             nid = engine.node_id(idx)
-            d = self.G.nodes[nid] if nid in self.G else {}
+            d = nodes[nid] if nid in self.G else {}
             kind = d.get("node_type")
             reranked.append({"node_id": nid, "node_type": kind,
                              "layer": 0 if kind == "entity" else (1 if kind == "summary" else 0),
-                             "semantic": float(res.out_sem[b, j]), "judge_overall": parse_judge(d.get("judge_scores")),
-                             "confidence": d.get("confidence"), "score": float(res.out_score[b, j]),
+                             "semantic": sem, "judge_overall": parse_judge(d.get("judge_scores")),
+                             "confidence": d.get("confidence"), "score": score,
                              "name": d.get("name"), "title": d.get("title")})
         if not return_cluster:
             return reranked
         expanded = []
-        for i in range(int(res.exp_count[b])):
-            idx = int(res.exp_nodes[b, i])
+        e = int(res.exp_count[b])
+        for idx, src, sem in zip(res.exp_nodes[b, :e].tolist(), res.exp_src[b, :e].tolist(),
+                                 res.exp_sem[b, :e].tolist()):
             nid = engine.node_id(idx)
-            src = int(res.exp_src[b, i])
             if src >= 0:
-                kind = self.G.nodes[nid].get("node_type") if idx < n_nodes else None
+                kind = nodes[nid].get("node_type") if idx < n_nodes else None
                 expanded.append({**seeds[src], "node_type": kind})
             else:
                 assumed = nat.NODE_TYPE_NAMES[-1 - src]
-                expanded.append({"node_id": nid, "semantic": float(res.exp_sem[b, i]),
+                expanded.append({"node_id": nid, "semantic": sem,
                                  "meta": {"expanded": True}, "node_type": assumed})
         return {"seeds": seeds, "expanded": expanded, "reranked": reranked}

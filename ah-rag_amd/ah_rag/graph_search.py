@@ -18,6 +18,7 @@ the environment's limit/break rules see the same neighbour sequence (SURVEY §8a
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
 from dataclasses import dataclass
@@ -42,15 +43,30 @@ SEARCH_DEFAULTS = {  # hierarchical_graph.py:37-47
 }
 
 
-def parse_judge(raw: Any) -> Optional[float]:
-    """`overall` of a node's judge_scores (JSON string or dict); None when absent or unparsable."""
-    if not raw:
-        return None
+def _parse_judge_obj(obj: Any) -> Optional[float]:
     try:
-        obj = json.loads(raw) if isinstance(raw, str) else raw
         return float(obj.get("overall", 0.0))
     except Exception:
         return None
+
+
+@functools.lru_cache(maxsize=1 << 16)
+def _parse_judge_str(raw: str) -> Optional[float]:
+    try:
+        return _parse_judge_obj(json.loads(raw))
+    except Exception:
+        return None
+
+
+def parse_judge(raw: Any) -> Optional[float]:
+    """`overall` of a node's judge_scores (JSON string or dict); None when absent or unparsable.
+    A string's value is a pure function of the string, so it is memoised (the batched search and
+    the environments parse the same few thousand strings over and over)."""
+    if not raw:
+        return None
+    if isinstance(raw, str):
+        return _parse_judge_str(raw)
+    return _parse_judge_obj(raw)
 
 
 def _as_float(x: Any) -> float:
