@@ -188,8 +188,9 @@ enum {
   kFlagNoQres = 2048,     // plan without the query-resident kernel
   kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
   kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
+  kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
 };
-constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv;
+constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
@@ -1125,6 +1126,284 @@ __global__ __launch_bounds__(512, 1) void topk_qkv_kernel(
 }
 
 // =============================================================================================
+// topk_t256_kernel (bf16/f16, k <= 16): 256 corpus rows x 256 queries per workgroup tile, 8 waves
+// (2 along rows x 4 along queries), each wave a 128 x 64 block of v_mfma_f32_16x16x32 (32
+// accumulator blocks = 128 VGPRs), one workgroup per CU, 64-deep k-steps through a 2-stage
+// 128-KiB buffer LDS-DMA ring that runs across tile boundaries. Against the 128 x 128 kernels:
+// 2x the MFMAs per staged byte and per LDS-read byte, and a k-step of 64 MFMAs per wave between
+// barriers instead of 16 (cdna_hip_programming.md: the 128^2 two-barrier structure tops out near
+// 0.9 PF/s; 256^2 tiles at one workgroup per CU are what go past it). Epilogue per tile: each
+// lane holds 4 query columns x 32 rows; per (query, 16-row group) the max against the query's
+// threshold; passing groups go through the lane's 64-B LDS slot, passing scores into a
+// per-(query, split, row half, lane quarter) candidate key buffer (a full buffer falls back to a
+// sorted list in private memory that raises the threshold). After the last tile each lane folds
+// its keys into a register list per query; the 4 lane quarters of a query merge by shuffles.
+// =============================================================================================
+namespace t256 {
+constexpr int kTR = 256, kTQ = 256;
+constexpr int kStage = (kTR + kTQ) * kRowBytes;  // 64 KiB: A (corpus) rows, then B (queries) rows
+constexpr int kOffSlot = 2 * kStage;             // 512 lanes x 64 B screening slots
+constexpr int kLds = kOffSlot + 512 * 64;        // 160 KiB
+static_assert(kLds <= 160 * 1024, "t256 LDS exceeds 160 KiB");
+}  // namespace t256
+
+__device__ __forceinline__ void mfma16(const u32x4& a, const u32x4& b, f32x4& acc, int dt) {
+  if (dt == DT_BF16)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
+                                                  0, 0);
+  else
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc, 0, 0,
+                                                 0);
+}
+
+template <int DT, int KCAP>
+__global__ __launch_bounds__(512, 1) void topk_t256_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ queries, int64_t row_stride, int n_rows,
+    int n_q, int n_ktiles, int n_row_tiles, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
+    const float* __restrict__ thr_init, int n_splits, int qblocks, int flags, uint64_t* __restrict__ cand_keys,
+    int cand_cap) {
+  static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2;  // 128-row half of the tile
+  const int wn = wave & 3;   // 64-query quarter of the block
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q0 = qb * t256::kTQ;
+  const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
+  const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
+
+  float thr[4];
+  uint64_t thk[4];
+  int nc[4];
+  // one register stash key per query slot: the first survivor of a query slot stays in a register,
+  // later ones go to the candidate buffer in memory; a store at a tile end would otherwise hold
+  // the next k-step's vmcnt(0) wait for its write acknowledgment
+  uint64_t stash[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int q = q0 + wn * 64 + nb * 16 + fr;
+    thr[nb] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+    thk[nb] = (q < n_q && thr[nb] != -INFINITY) ? (((uint64_t)ord_f32(thr[nb]) << 32) - 1) : 0;
+    nc[nb] = 0;
+    stash[nb] = 0;
+  }
+  // producer of query slot nb: (query, split, row half wm, lane quarter fq)
+  auto cbase = [&](int nb) __attribute__((always_inline)) {
+    const int q = q0 + wn * 64 + nb * 16 + fr;
+    return ((int64_t)q * (8 * n_splits) + 8 * split + 4 * wm + fq) * cand_cap;
+  };
+  volatile uint64_t Ls[4][KCAP];  // private memory: touched only when a candidate buffer is full
+#pragma unroll 1
+  for (int j = 0; j < 4 * KCAP; ++j) Ls[j / KCAP][j % KCAP] = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init reads retired before the ring counts
+
+  if (t_begin < t_end) {
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t tile_bytes = (uint32_t)(t256::kTR * row_stride);
+    const __amdgpu_buffer_rsrc_t q_rsrc = tile_rsrc(queries + (int64_t)q0 * row_stride, tile_bytes);
+    // DMA: wave w fills rows [32w, 32w + 32) of both the A and the B image, 8 rows per
+    // instruction; lane l lands at (row 8j + l/8, physical chunk l%8), loads logical chunk
+    // (l%8) ^ ((row >> 1) & 7). Rows 8j and 8j + 16 share the swizzle (soffset adds 16 rows).
+    uint32_t ld_off[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wave_u * 32 + 8 * j + (lane >> 3);
+      ld_off[j] = (uint32_t)(row * row_stride) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+    }
+    const uint32_t off16 = (uint32_t)(16 * row_stride);
+    auto issue = [&](int tile, int kt, int stage) __attribute__((always_inline)) {
+      const __amdgpu_buffer_rsrc_t c_rsrc = tile_rsrc(corpus + (int64_t)tile * t256::kTR * row_stride, tile_bytes);
+      unsigned char* dst = smem + stage * t256::kStage + wave_u * 32 * kRowBytes;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t so = kt * kRowBytes + (j >> 1) * off16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(c_rsrc, (__attribute__((address_space(3))) void*)(dst + j * 8 * kRowBytes),
+                                                 16, ld_off[j & 1], so, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            q_rsrc, (__attribute__((address_space(3))) void*)(dst + t256::kTR * kRowBytes + j * 8 * kRowBytes), 16,
+            ld_off[j & 1], so, 0, 0);
+      }
+    };
+    // fragment reads (16x16x32: lane l reads row l & 15, 16-B chunk 4s + l / 16 of the 64-deep
+    // k-step, XOR-swizzled by bits 1-3 of the row)
+    const int x = (fr >> 1) & 7;
+    const uint32_t fo0 = (uint32_t)(fr * kRowBytes + (((0 + fq) ^ x) << 4));
+    const uint32_t fo1 = (uint32_t)(fr * kRowBytes + (((4 + fq) ^ x) << 4));
+
+    f32x4 acc[8][4];
+    float* slot = reinterpret_cast<float*>(smem + t256::kOffSlot) + tid * 16;
+
+    auto list_push = [&](int nb, uint64_t key) {
+      int j = KCAP - 1;
+#pragma unroll 1
+      while (j > 0 && Ls[nb][j - 1] < key) {
+        Ls[nb][j] = Ls[nb][j - 1];
+        --j;
+      }
+      Ls[nb][j] = key;
+      const uint64_t kth = Ls[nb][k_out - 1];
+      if (kth > thk[nb]) {
+        thk[nb] = kth;
+        thr[nb] = key_score(kth);
+      }
+    };
+
+    issue(t_begin, 0, 0);
+    int c = 0;  // global k-step counter (stage = c & 1)
+    for (int t = t_begin; t < t_end; ++t) {
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kt = 0; kt < n_ktiles; ++kt, ++c) {
+        // top of step c: this wave's DMA of step c landed (the only one in flight), then the
+        // barrier: everyone's landed, everyone is done reading step c - 1's stage
+        if (!(flags & kFlagNoWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (!(flags & kFlagNoLoads)) {
+          if (kt + 1 < n_ktiles)
+            issue(t, kt + 1, (c + 1) & 1);
+          else if (t + 1 < t_end)
+            issue(t + 1, 0, (c + 1) & 1);
+        }
+        const unsigned char* st = smem + (c & 1) * t256::kStage;
+        const unsigned char* abase = st + (wm * 128) * kRowBytes;
+        const unsigned char* bbase = st + (t256::kTR + wn * 64) * kRowBytes;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const uint32_t fo = s ? fo1 : fo0;
+          u32x4 b[4];
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const u32x4*>(bbase + nb * 16 * kRowBytes + fo);
+#pragma unroll
+          for (int mb = 0; mb < 8; ++mb) {
+            const u32x4 a = *reinterpret_cast<const u32x4*>(abase + mb * 16 * kRowBytes + fo);
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) mfma16(a, b[nb], acc[mb][nb], DT);
+          }
+        }
+      }
+      if (flags & kFlagSkipEpilogue) continue;
+      // ---- tile end: (query slot nb, row half mh) groups = acc[4 mh .. 4 mh + 3][nb], 16 rows
+      const int r0 = t * t256::kTR + wm * 128;
+      uint32_t gmask = 0;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+          float m = acc[4 * mh][nb][0];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) m = fmaxf(m, acc[4 * mh + u][nb][i]);
+          gmask |= (m >= thr[nb] ? 1u : 0u) << (nb * 2 + mh);
+        }
+      if (flags & kFlagMaxOnly) {  // ablation: group maxima only (wrong results)
+        if (gmask == 0xFFu && thr[0] == 1234.5f) part_keys[0] = 1;
+        continue;
+      }
+      while (__ballot(gmask != 0)) {
+        const int sel = gmask ? __builtin_ctz(gmask) : -1;
+        gmask &= gmask - 1;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          if (sel == g) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) *reinterpret_cast<f32x4*>(slot + 4 * u) = acc[4 * (g & 1) + u][g >> 1];
+          }
+        }
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          if (sel >= 0 && (sel >> 1) == nb) {
+            const int rb = r0 + (sel & 1) * 64 + fq * 4;  // value 4u + i: row rb + 16u + i
+            uint32_t pm = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * u);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) pm |= (v4[i] >= thr[nb] && rb + 16 * u + i < n_rows ? 1u : 0u) << (4 * u + i);
+            }
+            while (pm) {
+              const int r = __builtin_ctz(pm);
+              pm &= pm - 1;
+              const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + 16 * (r >> 2) + (r & 3)));
+              if (key > thk[nb]) {
+                if (stash[nb] == 0) {
+                  stash[nb] = key;
+                } else if (nc[nb] < cand_cap) {
+                  cand_keys[cbase(nb) + nc[nb]] = key;
+                  ++nc[nb];
+                } else {
+                  list_push(nb, key);
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+    if (flags & kFlagSkipEpilogue) {
+      float sink = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) sink += acc[mb][nb][0] + acc[mb][nb][3];
+      if (sink == 1234.5678f) part_keys[0] = 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
+  }
+
+  // per query slot: fold the candidate keys into a register list, merge the 4 lane quarters
+  // (lanes fr, fr + 16, fr + 32, fr + 48: disjoint rows of one query), write one list per
+  // (query, split, row half)
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int q = q0 + wn * 64 + nb * 16 + fr;
+    uint64_t L[KCAP];
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[j] = Ls[nb][j];
+    if (stash[nb]) list_insert<KCAP>(L, stash[nb]);
+    const int n = nc[nb];
+    const int64_t cb = q < n_q ? cbase(nb) : 0;
+    for (int g0 = 0; g0 < n; g0 += 8) {
+      uint64_t c8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c8[u] = g0 + u < n ? cand_keys[cb + g0 + u] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c8[u]) list_insert<KCAP>(L, c8[u]);
+    }
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      uint64_t P[KCAP];
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) P[j] = shfl_xor_u64(L[j], m);
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) list_insert<KCAP>(L, P[j]);
+    }
+    if (fq == 0 && q < n_q) {
+      uint64_t* dst = part_keys + ((int64_t)q * (2 * n_splits) + 2 * split + wm) * k_out;
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j)
+        if (j < k_out) dst[j] = L[j];
+    }
+  }
+}
+
+// =============================================================================================
 // lane kernel: waves arranged WR (along corpus rows) x WQ (along queries); each wave owns NB
 // 32-row blocks x BJ 32-query blocks of the workgroup tile (MFMA 32x32: corpus rows are the A
 // operand, queries B), so every lane's accumulator columns are BJ queries and the lane keeps
@@ -1981,7 +2260,8 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 // ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
 // 3 = 128x128 lane-local tile kernel, 5 = query-resident kernel (dimension halves over wave pairs);
 // 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed)
-enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5 };
+enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
+       KERNEL_T256 = 6 };
 
 struct SearchPlan {
   int kernel;
@@ -2020,6 +2300,18 @@ bool qkv_ok(const ahr_index* ix, int B, int k) {
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
+  if (k <= 16 && ix->dtype != AHR_F32 && (ix->debug_flags & kFlagT256)) {
+    // 256x256 tiles, one workgroup per CU: one wave of 256 workgroups
+    p.kernel = KERNEL_T256;
+    p.qblocks = (int)cdiv(B, t256::kTQ);
+    p.n_row_tiles = (int)cdiv(ix->count, t256::kTR);
+    int want = std::max(1, 256 / p.qblocks);
+    want = std::min(want, std::max(1, p.n_row_tiles));
+    p.xcd_remap = want >= 8;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    return p;
+  }
   if (qkv_ok(ix, B, k)) {
     // one workgroup per CU (512 VGPRs per lane): one wave of 256 workgroups
     p.kernel = KERNEL_QKV;
@@ -2088,8 +2380,10 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
   const int64_t qblocks = cdiv(B, kTileQ);
   const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlots128, qblocks)), 8) * 8;
   const int64_t wide_splits = std::max<int64_t>(1, 512 / cdiv(B, 128));  // >= any plan's
-  const int64_t p_need =
-      (int64_t)B * std::max<int64_t>(std::max(max_splits, wide_splits), kSampleMax / kTileRows) * k;
+  const int64_t t256_lists = 2 * std::max<int64_t>(1, 256 / cdiv(B, 256));  // (split, row half) lists
+  const int64_t p_need = (int64_t)B *
+                         std::max<int64_t>(std::max(std::max(max_splits, wide_splits), t256_lists), kSampleMax / kTileRows) *
+                         k;
   if (p_need > ix->part_cap) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
     ix->part = nullptr;
@@ -2165,7 +2459,10 @@ void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B
 // the C2 survivor rate (~1 row per producer) many times over; a full buffer falls back to the
 // lane's private list inside the kernel, so the cap only trades memory for speed.
 inline int qkv_cand_cap(const SearchPlan& p) { return (int)std::min(64, std::max(16, p.tiles_per_split)); }
-inline int64_t cand_bytes(int B, const SearchPlan& p) { return (int64_t)B * 4 * p.n_splits * qkv_cand_cap(p) * 8; }
+inline int64_t cand_bytes(int B, const SearchPlan& p) {
+  const int64_t prod = p.kernel == KERNEL_T256 ? 8 : 4;  // candidate producers per (query, split)
+  return (int64_t)B * prod * p.n_splits * qkv_cand_cap(p) * 8;
+}
 
 int ensure_cand(ahr_index* ix, int64_t bytes) {
   if (bytes <= ix->cand_cap) return AHR_OK;
@@ -2190,6 +2487,21 @@ void launch_qkv(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), lds, s, ix->rows, ix->qbuf,
                      ix->row_stride, n_rows, B, p.n_row_tiles, row_base, k, ix->part, thr, p.n_splits, p.qblocks,
                      flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
+}
+
+template <int DT, int KCAP>
+void launch_t256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                 const float* thr, int flags, hipStream_t s) {
+  constexpr auto kern = &topk_t256_kernel<DT, KCAP>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              t256::kLds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), t256::kLds, s, ix->rows, ix->qbuf,
+                     ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes, p.n_row_tiles, row_base, k, ix->part,
+                     thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
 
 template <int DT, int NKT>
@@ -2235,6 +2547,15 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
+    if (p.kernel == KERNEL_T256) {
+      if (k <= 8)
+        launch_t256<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s);
+      else if (k <= 12)
+        launch_t256<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s);
+      else
+        launch_t256<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s);
+      return;
+    }
     if (p.kernel == KERNEL_QKV) {
       if (ix->d_pad * ix->elem / kRowBytes == 12)
         launch_qkv_k<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s);
@@ -2363,7 +2684,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     }
   }
   SearchPlan p = plan_search(ix, B, k);
-  if (p.kernel == KERNEL_QKV && ix->count > 0) {
+  if ((p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256) && ix->count > 0) {
     st = ensure_cand(ix, cand_bytes(B, p));
     if (st) return st;
   }
@@ -2379,7 +2700,8 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   }
   prof_mark(ix, 3, s);
   {
-    const int lists = (p.kernel == KERNEL_QKV ? 2 : 1) * p.n_splits;  // qkv: one list per (split, half)
+    // qkv: one list per (split, dimension half); t256: one per (split, row half)
+    const int lists = (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 ? 2 : 1) * p.n_splits;
     launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
   }
   prof_mark(ix, 4, s);
@@ -2621,7 +2943,7 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
   // candidate groups of the query-resident plan at the current corpus size
   for (int kk = 1; kk <= max_k; kk = kk < 8 ? 8 : kk + 8) {
     const SearchPlan p = plan_search(ix, max_batch, kk);
-    if (p.kernel == KERNEL_QKV) {
+    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256) {
       st = ensure_cand(ix, cand_bytes(max_batch, p));
       if (st) return st;
     }

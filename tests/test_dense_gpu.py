@@ -406,3 +406,28 @@ def test_large_k_ties_order_by_row(cuda):
     es, er = dr.topk(C, Q, 100, mode="fma")
     np.testing.assert_array_equal(r, er)
     np.testing.assert_array_equal(s, es.astype(np.float32))
+
+
+# ---- 256 x 256 16x16x32 kernel (debug flag 32768 while it is not a default plan) ----------------
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n,d,B,k,sample", [
+    (40001, 768, 1024, 10, 8192), (40001, 768, 1024, 10, 0), (33000, 384, 300, 16, 8192),
+    (300, 768, 1, 1, 0), (1000, 128, 257, 8, 0), (90000, 768, 2048, 5, 8192)])
+def test_t256_matches_tilelane(cuda, dtype, n, d, B, k, sample):
+    """16x16x32 MFMAs sum each 32-deep slice inside one instruction: scores within 2e-6 of the
+    32x32x16 chain, rows equal except near-ties; splits with no tiles, ragged blocks, no seed."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(91 + n + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    ix.set_sample_rows(sample)
+    ix.set_debug_flags(32768)
+    assert ix.plan(B, k)["kernel"] == "t256"
+    a = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(32)
+    b = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.close()
+    _close_topk(a, b)
