@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(512, 1) void topk_qkv_kernel(
 // barriers instead of 16 (cdna_hip_programming.md: the 128^2 two-barrier structure tops out near
 // 0.9 PF/s; 256^2 tiles at one workgroup per CU are what go past it). Epilogue per tile: each
 // lane holds 4 query columns x 32 rows; per (query, 16-row group) the max against the query's
-// threshold; passing groups go through the lane's 64-B LDS slot, passing scores into a
+// threshold; passing groups are scanned straight from the accumulators, passing scores into a
 // per-(query, split, row half, lane quarter) candidate key buffer (a full buffer falls back to a
 // sorted list in private memory that raises the threshold). After the last tile each lane folds
 // its keys into a register list per query; the 4 lane quarters of a query merge by shuffles.
@@ -1244,7 +1244,6 @@ __global__ __launch_bounds__(512, 1) void topk_t256_kernel(
     const uint32_t fo1 = (uint32_t)(fr * kRowBytes + (((4 + fq) ^ x) << 4));
 
     f32x4 acc[8][4];
-    float* slot = reinterpret_cast<float*>(smem + t256::kOffSlot) + tid * 16;
 
     auto list_push = [&](int nb, uint64_t key) {
       int j = KCAP - 1;
@@ -1315,40 +1314,36 @@ __global__ __launch_bounds__(512, 1) void topk_t256_kernel(
         if (gmask == 0xFFu && thr[0] == 1234.5f) part_keys[0] = 1;
         continue;
       }
-      while (__ballot(gmask != 0)) {
-        const int sel = gmask ? __builtin_ctz(gmask) : -1;
-        gmask &= gmask - 1;
+      // passing groups, one static group at a time (skipped unless some lane passes it): the
+      // pass mask and the passing values come straight from the accumulators (select chain), no
+      // LDS round trip
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          if (sel == g) {
+      for (int g = 0; g < 8; ++g) {
+        const int nb = g >> 1, mh = g & 1;
+        if (!__ballot((gmask >> g) & 1u)) continue;
+        if ((gmask >> g) & 1u) {
+          const int rb = r0 + mh * 64 + fq * 4;  // value 4u + i: row rb + 16u + i
+          uint32_t pm = 0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) *reinterpret_cast<f32x4*>(slot + 4 * u) = acc[4 * (g & 1) + u][g >> 1];
-          }
-        }
+          for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb) {
-          if (sel >= 0 && (sel >> 1) == nb) {
-            const int rb = r0 + (sel & 1) * 64 + fq * 4;  // value 4u + i: row rb + 16u + i
-            uint32_t pm = 0;
+            for (int i = 0; i < 4; ++i)
+              pm |= (acc[4 * mh + u][nb][i] >= thr[nb] && rb + 16 * u + i < n_rows ? 1u : 0u) << (4 * u + i);
+          while (pm) {
+            const int r = __builtin_ctz(pm);
+            pm &= pm - 1;
+            float v = acc[4 * mh][nb][0];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * u);
-#pragma unroll
-              for (int i = 0; i < 4; ++i) pm |= (v4[i] >= thr[nb] && rb + 16 * u + i < n_rows ? 1u : 0u) << (4 * u + i);
-            }
-            while (pm) {
-              const int r = __builtin_ctz(pm);
-              pm &= pm - 1;
-              const uint64_t key = make_key(slot[r], row_base + (uint32_t)(rb + 16 * (r >> 2) + (r & 3)));
-              if (key > thk[nb]) {
-                if (stash[nb] == 0) {
-                  stash[nb] = key;
-                } else if (nc[nb] < cand_cap) {
-                  cand_keys[cbase(nb) + nc[nb]] = key;
-                  ++nc[nb];
-                } else {
-                  list_push(nb, key);
-                }
+            for (int rr = 1; rr < 16; ++rr) v = (r == rr) ? acc[4 * mh + (rr >> 2)][nb][rr & 3] : v;
+            const uint64_t key = make_key(v, row_base + (uint32_t)(rb + 16 * (r >> 2) + (r & 3)));
+            if (key > thk[nb]) {
+              if (stash[nb] == 0) {
+                stash[nb] = key;
+              } else if (nc[nb] < cand_cap) {
+                cand_keys[cbase(nb) + nc[nb]] = key;
+                ++nc[nb];
+              } else {
+                list_push(nb, key);
               }
             }
           }
