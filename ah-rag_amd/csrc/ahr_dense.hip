@@ -1142,8 +1142,7 @@ __global__ __launch_bounds__(512, 1) void topk_qkv_kernel(
 namespace t256 {
 constexpr int kTR = 256, kTQ = 256;
 constexpr int kStage = (kTR + kTQ) * kRowBytes;  // 64 KiB: A (corpus) rows, then B (queries) rows
-constexpr int kOffSlot = 2 * kStage;             // 512 lanes x 64 B screening slots
-constexpr int kLds = kOffSlot + 512 * 64;        // 160 KiB
+constexpr int kLds = 2 * kStage;                 // 128 KiB
 static_assert(kLds <= 160 * 1024, "t256 LDS exceeds 160 KiB");
 }  // namespace t256
 
