@@ -2047,6 +2047,54 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float v) {
 // fp32 storage permutation inside each group of 8: position of logical lane j.
 __device__ __forceinline__ int f32_perm(int j) { return (j & ~7) | ((j & 1) << 2) | ((j >> 1) & 3); }
 
+// Fast path of convert_rows_kernel (bf16/f16 rows up to 1024 wide, dim % 4 == 0), one wave per
+// row: the whole row in flight at once (clamped addresses, masked after); the general loop waits
+// on each 1-KiB piece in turn. Same arithmetic and order as the loop: the per-lane fma chain in j
+// order, then the butterfly. `row` may be global or LDS (topk_small_kernel converts its queries
+// in place); [0, d_pad) is written in full, zeros past dim.
+__device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, int dim, int normalize,
+                                                 uint8_t* row, int d_pad, int dt, int lane) {
+  f32x4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = 4 * lane + 256 * u;
+    v[u] = *reinterpret_cast<const f32x4*>(x + (j < dim ? j : dim - 4));
+    if (j >= dim) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float nrm = 1.f;
+  if (normalize) {
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s = fmaf(v[u][0], v[u][0], s); s = fmaf(v[u][1], v[u][1], s);
+      s = fmaf(v[u][2], v[u][2], s); s = fmaf(v[u][3], v[u][3], s);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    nrm = fmaxf(sqrtf(s), 1e-12f);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = 4 * lane + 256 * u;
+    if (j >= d_pad) break;
+    f32x4 w4 = v[u];
+    if (normalize) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w4[e] = w4[e] / nrm;
+    }
+    if (dt == DT_BF16) {
+      uint2 w;
+      w.x = (uint32_t)f32_to_bf16_rne(w4[0]) | ((uint32_t)f32_to_bf16_rne(w4[1]) << 16);
+      w.y = (uint32_t)f32_to_bf16_rne(w4[2]) | ((uint32_t)f32_to_bf16_rne(w4[3]) << 16);
+      *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
+    } else {
+      _Float16* o = reinterpret_cast<_Float16*>(row) + j;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (_Float16)w4[e];
+    }
+  }
+}
+
 // fp32 rows -> storage rows (one wave per row): optional L2 normalisation, dtype conversion,
 // zero padding to d_pad, fp32 lane permutation. Lanes move 4 consecutive elements at a time.
 __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restrict__ src, int64_t n,
@@ -2061,50 +2109,8 @@ __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restri
   const float* x = src + i * dim;
   const bool vec = (dim & 3) == 0;
   if (vec && d_pad <= 1024 && dt != DT_F32) {
-    // Fast path (bf16/f16 rows up to 1024 wide): the whole row in flight at once (clamped
-    // addresses, masked after); the general loop below waits on each 1-KiB piece in turn. Same
-    // arithmetic and order as the loop: the per-lane fma chain in j order, then the butterfly.
-    f32x4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = 4 * lane + 256 * u;
-      v[u] = *reinterpret_cast<const f32x4*>(x + (j < dim ? j : dim - 4));
-      if (j >= dim) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    float nrm = 1.f;
-    if (normalize) {
-      float s = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        s = fmaf(v[u][0], v[u][0], s); s = fmaf(v[u][1], v[u][1], s);
-        s = fmaf(v[u][2], v[u][2], s); s = fmaf(v[u][3], v[u][3], s);
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-      nrm = fmaxf(sqrtf(s), 1e-12f);
-    }
     const int64_t slot = slots ? slots[i] : start + i;
-    uint8_t* row = dst + slot * row_stride;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = 4 * lane + 256 * u;
-      if (j >= d_pad) break;
-      f32x4 w4 = v[u];
-      if (normalize) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w4[e] = w4[e] / nrm;
-      }
-      if (dt == DT_BF16) {
-        uint2 w;
-        w.x = (uint32_t)f32_to_bf16_rne(w4[0]) | ((uint32_t)f32_to_bf16_rne(w4[1]) << 16);
-        w.y = (uint32_t)f32_to_bf16_rne(w4[2]) | ((uint32_t)f32_to_bf16_rne(w4[3]) << 16);
-        *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
-      } else {
-        _Float16* o = reinterpret_cast<_Float16*>(row) + j;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (_Float16)w4[e];
-      }
-    }
+    convert_row_fast(x, dim, normalize, dst + slot * row_stride, d_pad, dt, lane);
     return;
   }
   float nrm = 1.f;
@@ -2169,6 +2175,216 @@ __global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restric
       v = reinterpret_cast<const float*>(row)[f32_perm(j)];
     }
     out[i * dim + j] = v;
+  }
+}
+
+
+// =============================================================================================
+// topk_small_kernel (B <= 16, bf16/f16, k <= 16): every corpus row is read once and scored
+// against at most 16 queries, so the launch is bound by the corpus stream (HBM / MALL), not by
+// MFMA, and a 128-query tile wastes 7/8 of its work. No threshold pre-pass and no LDS staging
+// of the corpus: the (at most) 16 query rows are converted from fp32 straight into LDS by the
+// workgroup (convert_row_fast: the convert kernel's arithmetic, so the same rounded queries),
+// and each of the 16 waves streams 16-row corpus blocks straight into registers as the A
+// operand of v_mfma_f32_16x16x32 (lane l: row l & 15, 16-B chunk l / 16 of each 32-deep step,
+// the t256 kernel's fragment map, so the scores are bitwise those of its k-ordered chain).
+// A wave's work is a sequence of (block, 8 k-steps) items in two register sets: the next item's
+// loads (the first one before the query staging) fly under the current item's MFMAs and the
+// block epilogue; 16 waves per CU keep up to 256 KiB of loads in flight. Epilogue: lane l holds query l & 15 at rows
+// 4 (l / 16) + i of the block and keeps a register list for it (the k-th key is its threshold);
+// at the end the 64 lists of each query (16 waves x 4 lane quarters) merge through LDS, one wave
+// per query, into one list per (query, split).
+// =============================================================================================
+namespace small {
+constexpr int kMaxQ = 16;
+constexpr int kWaves = 16;
+constexpr int kThreads = kWaves * 64;
+constexpr int kKC = 8;  // 32-deep k-steps per work item (one register set)
+constexpr int kPitchPad = 16;  // query rows in LDS: pitch = row bytes + 16 (conflict-free reads)
+inline int lds_bytes(int64_t row_stride, int kcap) {
+  const int64_t q = kMaxQ * (row_stride + kPitchPad);
+  const int64_t l = (int64_t)kMaxQ * 4 * kWaves * kcap * 8;
+  return (int)(q > l ? q : l);
+}
+}  // namespace small
+
+template <int DT, int KCAP>
+__global__ __launch_bounds__(small::kThreads, 1) void topk_small_kernel(
+    const uint8_t* __restrict__ corpus, const float* __restrict__ qsrc, int dim, int normalize,
+    const uint8_t* __restrict__ qconv, int64_t row_stride, int d_pad, int n_rows, int n_q, int n_steps,
+    int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys) {
+  static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  const int split = blockIdx.x;
+  const int pitch = (int)row_stride + small::kPitchPad;
+
+  const int n_blocks = (n_rows + 15) >> 4;
+  const int b_begin = (int)((int64_t)split * n_blocks / n_splits);
+  const int b_end = (int)((int64_t)(split + 1) * n_blocks / n_splits);
+  // the wave's work is a sequence of items (16-row block, 8 k-steps); two register sets keep the
+  // next item's loads in flight under the current item's MFMAs, across block boundaries
+  auto load_item = [&](u32x4 (&A)[small::kKC], int blk, int s0) __attribute__((always_inline)) {
+    const uint8_t* arow = corpus + (int64_t)(blk * 16 + fr) * row_stride + fq * 16 + s0 * 64;
+#pragma unroll
+    for (int j = 0; j < small::kKC; ++j)
+      if (s0 + j < n_steps) A[j] = *reinterpret_cast<const u32x4*>(arow + j * 64);
+  };
+  u32x4 A0[small::kKC], A1[small::kKC];
+  int cb = b_begin + wave, cs = 0;
+  if (cb < b_end) load_item(A0, cb, 0);  // in flight while the queries are staged
+
+  // queries into LDS: converted from fp32 here (wave w: query w), or copied from the query buffer
+  if (qsrc) {
+    if (wave < n_q) convert_row_fast(qsrc + (int64_t)wave * dim, dim, normalize, smem + wave * pitch, d_pad, DT, lane);
+  } else {
+    const int chunks = (int)(row_stride >> 4);
+    for (int i = tid; i < n_q * chunks; i += small::kThreads) {
+      const int r = i / chunks;
+      const int c = i - r * chunks;
+      *reinterpret_cast<u32x4*>(smem + r * pitch + c * 16) =
+          *reinterpret_cast<const u32x4*>(qconv + (int64_t)r * row_stride + c * 16);
+    }
+  }
+  __syncthreads();
+
+  uint64_t L[KCAP];
+#pragma unroll
+  for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  uint64_t thk = 0;     // the list's k-th key (0 while it holds fewer than k)
+  float thr = -INFINITY;
+  const bool qok = fr < n_q;
+  const unsigned char* qrow = smem + fr * pitch + fq * 16;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // one item: issue the next item's loads into N, MFMAs over C, the block's epilogue after its
+  // last item; returns false when the wave is done
+  auto step = [&](u32x4 (&C)[small::kKC], u32x4 (&N)[small::kKC]) __attribute__((always_inline)) {
+    int nb = cb, ns = cs + small::kKC;
+    if (ns >= n_steps) {
+      ns = 0;
+      nb += small::kWaves;
+    }
+    if (nb < b_end) load_item(N, nb, ns);
+#pragma unroll
+    for (int j = 0; j < small::kKC; ++j)
+      if (cs + j < n_steps) mfma16(C[j], *reinterpret_cast<const u32x4*>(qrow + (cs + j) * 64), acc, DT);
+    if (ns == 0) {
+      const int r0 = cb * 16 + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (qok && acc[i] >= thr && r0 + i < n_rows) {
+          const uint64_t key = make_key(acc[i], row_base + (uint32_t)(r0 + i));
+          if (key > thk) {
+            list_insert<KCAP>(L, key);
+            thk = list_at<KCAP>(L, k_out - 1);
+            thr = thk ? key_score(thk) : -INFINITY;
+          }
+        }
+      }
+      acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    cb = nb;
+    cs = ns;
+    return cb < b_end;
+  };
+  if (cb < b_end) {
+    while (step(A0, A1) && step(A1, A0)) {
+    }
+  }
+
+  // 64 lists per query -> LDS [query][wave * 4 + quarter][KCAP] -> one wave per query merges
+  __syncthreads();  // every wave is done reading the queries (the lists overlay them)
+  uint64_t* lists = reinterpret_cast<uint64_t*>(smem);
+  if (qok) {
+    uint64_t* dst = lists + ((int64_t)fr * (4 * small::kWaves) + wave * 4 + fq) * KCAP;
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) dst[j] = L[j];
+  }
+  __syncthreads();
+  const int q = wave;
+  if (q < n_q) {
+    const uint64_t* src = lists + ((int64_t)q * (4 * small::kWaves) + lane) * KCAP;
+    uint64_t M[KCAP];
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) M[j] = src[j];
+    uint64_t mine = 0;  // lane j keeps the j-th winner
+    for (int j = 0; j < k_out; ++j) {
+      const uint64_t best = wave_max_u64(M[0]);
+      if (best != 0 && M[0] == best) {
+#pragma unroll
+        for (int t = 0; t < KCAP - 1; ++t) M[t] = M[t + 1];
+        M[KCAP - 1] = 0;
+      }
+      if (lane == j) mine = best;
+    }
+    if (lane < k_out) part_keys[((int64_t)q * n_splits + split) * k_out + lane] = mine;
+  }
+}
+
+// k-way merge of up to 512 sorted lists per query (n_lists * k_in <= 8192), one 256-thread
+// workgroup per query: every key comes into LDS with coalesced loads in one go (a head-advancing
+// merge over global memory pays one dependent L2 latency per output), then k rounds of a
+// block-wide max over the list heads (thread t owns lists t and t + 256).
+constexpr int kMergeBlockKeys = 8192;
+__global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __restrict__ in, int n_lists, int k_in,
+                                                          int k, float* __restrict__ scores,
+                                                          int32_t* __restrict__ rows,
+                                                          uint64_t* __restrict__ keys_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* kb = reinterpret_cast<uint64_t*>(smem);
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int n = n_lists * k_in;
+  const uint64_t* src = in + (int64_t)q * n;
+  // all loads in flight at once: a load -> LDS store loop waits one L2 latency per iteration
+  constexpr int kPer = kMergeBlockKeys / 256;
+  uint64_t v[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = tid + 256 * u;
+    if (256 * u < n) v[u] = src[i < n ? i : n - 1];  // 256 u < n is block-uniform
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = tid + 256 * u;
+    if (i < n) kb[i] = v[u];
+  }
+  uint64_t* wmax = kb + n;  // [2 round parities][4 waves]
+  __syncthreads();
+  const int l0 = tid, l1 = tid + 256;
+  int p0 = 0, p1 = 0;
+  uint64_t h0 = (l0 < n_lists && k_in > 0) ? kb[l0 * k_in] : 0;
+  uint64_t h1 = (l1 < n_lists && k_in > 0) ? kb[l1 * k_in] : 0;
+  for (int j = 0; j < k; ++j) {
+    const uint64_t wm = wave_max_u64(h0 > h1 ? h0 : h1);
+    // parity slots: a wave writing round j + 2 has passed round j + 1's barrier, which every
+    // wave reaches only after reading round j
+    if (lane == 0) wmax[(j & 1) * 4 + wave] = wm;
+    __syncthreads();
+    uint64_t best = wmax[(j & 1) * 4];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) best = max_u64(best, wmax[(j & 1) * 4 + w]);
+    if (best != 0) {
+      if (h0 == best) {
+        ++p0;
+        h0 = p0 < k_in ? kb[l0 * k_in + p0] : 0;
+      } else if (h1 == best) {
+        ++p1;
+        h1 = p1 < k_in ? kb[l1 * k_in + p1] : 0;
+      }
+    }
+    if (tid == 0) {
+      const int64_t o = (int64_t)q * k + j;
+      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
+      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
+      if (keys_out) keys_out[o] = best;
+    }
   }
 }
 
@@ -2253,9 +2469,10 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 
 // ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
 // 3 = 128x128 lane-local tile kernel, 5 = query-resident kernel (dimension halves over wave pairs);
-// 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed)
+// 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed), 6 = 256x256 16x16x32
+// kernel (opt-in), 7 = small-batch streaming kernel (B <= 16)
 enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
-       KERNEL_T256 = 6 };
+       KERNEL_T256 = 6, KERNEL_SMALL = 7 };
 
 struct SearchPlan {
   int kernel;
@@ -2291,9 +2508,27 @@ bool qkv_ok(const ahr_index* ix, int B, int k) {
   return B >= 2048 && B <= 8192 && ix->sample_rows > 0 && ix->count <= 32 * (int64_t)ix->sample_rows;
 }
 
+// The small-batch streaming kernel: B <= 16, bf16/f16, k <= 16, the 16 query rows (or the
+// 64 x KCAP lists per query of the end merge) within LDS; not under an explicit kernel flag.
+bool small_ok(const ahr_index* ix, int B, int k) {
+  if (B > small::kMaxQ || k > 16 || ix->dtype == AHR_F32) return false;
+  if (ix->debug_flags & kKernelFlags) return false;
+  return small::lds_bytes(ix->row_stride, 16) <= 160 * 1024;
+}
+
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
+  if (small_ok(ix, B, k)) {
+    // one workgroup (16 waves) per CU, at least one 16-row block per wave
+    p.kernel = KERNEL_SMALL;
+    p.qblocks = 1;
+    p.n_row_tiles = (int)cdiv(ix->count, 16);
+    p.n_splits = (int)std::max<int64_t>(1, std::min<int64_t>(256, cdiv(p.n_row_tiles, small::kWaves)));
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    p.xcd_remap = false;
+    return p;
+  }
   if (k <= 16 && ix->dtype != AHR_F32 && (ix->debug_flags & kFlagT256)) {
     // 256x256 tiles, one workgroup per CU: one wave of 256 workgroups
     p.kernel = KERNEL_T256;
@@ -2521,11 +2756,43 @@ void launch_lane_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, 
     launch_lane<DT, 16, NB, BJ, WR, WQ, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
 }
 
+template <int DT, int KCAP>
+void launch_small(const ahr_index* ix, const SearchPlan& p, const float* q, int normalize_q, int B, int k,
+                  uint32_t row_base, hipStream_t s) {
+  constexpr auto kern = &topk_small_kernel<DT, KCAP>;
+  const int lds = small::lds_bytes(ix->row_stride, KCAP);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::kThreads), lds, s, ix->rows, q, ix->dim,
+                     normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, (int)ix->count, B,
+                     (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part);
+}
+
+// queries converted inside topk_small_kernel (convert_row_fast's shape) instead of by the convert kernel
+inline bool small_fuses_convert(const ahr_index* ix) { return (ix->dim & 3) == 0 && ix->d_pad <= 1024; }
+
 template <int DT>
-void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base,
-                   hipStream_t s) {
+void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const float* q,
+                   int normalize_q, hipStream_t s) {
   const float* thr = nullptr;
   prof_mark(ix, 1, s);
+  if constexpr (DT != DT_F32) {
+    if (p.kernel == KERNEL_SMALL) {
+      prof_mark(ix, 2, s);
+      const float* qs = small_fuses_convert(ix) ? q : nullptr;
+      if (k <= 8)
+        launch_small<DT, 8>(ix, p, qs, normalize_q, B, k, row_base, s);
+      else if (k <= 12)
+        launch_small<DT, 12>(ix, p, qs, normalize_q, B, k, row_base, s);
+      else
+        launch_small<DT, 16>(ix, p, qs, normalize_q, B, k, row_base, s);
+      return;
+    }
+  }
   const int S = ix->sample_rows;
   if (S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
     // Threshold pre-pass: score the first S rows, take each query's k-th best.
@@ -2592,6 +2859,17 @@ void launch_merge(const uint64_t* in, int B, int n_lists, int k_in, int k, float
       hipLaunchKernelGGL((merge_lane_lists_kernel<16>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
     else
       hipLaunchKernelGGL((merge_lane_lists_kernel<32>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+    return;
+  }
+  if (n_lists <= 512 && n_lists * k_in <= kMergeBlockKeys) {
+    static bool attr_set = false;  // up to 64 KiB + 64 B of dynamic LDS
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_block_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kMergeBlockKeys * 8 + 64);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(merge_block_kernel, dim3(B), dim3(256), (size_t)n_lists * k_in * 8 + 64, s, in, n_lists, k_in,
+                       k, scores, rows, keys_out);
     return;
   }
   if (n_lists <= 64 * kHeadSlots) {
@@ -2667,9 +2945,11 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   int st = ensure_query_ws(ix, B, k, s);
   if (st) return st;
   prof_mark(ix, 0, s);
-  hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
-                     (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
-                     ix->row_stride, ix->d_pad, ix->dtype);
+  const bool small_plan = k <= AHR_MAX_K && ix->count > 0 && plan_search(ix, B, k).kernel == KERNEL_SMALL;
+  if (!(small_plan && small_fuses_convert(ix)))
+    hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
+                       (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
+                       ix->row_stride, ix->d_pad, ix->dtype);
   if (k > AHR_MAX_K) {
     switch (ix->dtype) {
       case AHR_BF16: return run_query_large_k<DT_BF16>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);
@@ -2684,9 +2964,9 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   }
   if (ix->count > 0) {
     switch (ix->dtype) {
-      case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, s); break;
-      case AHR_F16: launch_search<DT_F16>(ix, p, B, k, (uint32_t)row_base, s); break;
-      default: launch_search<DT_F32>(ix, p, B, k, (uint32_t)row_base, s); break;
+      case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, s); break;
+      case AHR_F16: launch_search<DT_F16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, s); break;
+      default: launch_search<DT_F32>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, s); break;
     }
   } else {
     prof_mark(ix, 1, s);

@@ -247,8 +247,13 @@ def main() -> None:
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
         plan = local.plan(B, k)
         kname = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
-                 "tilelane128": "topk_tilelane_kernel",
+                 "tilelane128": "topk_tilelane_kernel", "t256": "topk_t256_kernel",
+                 "small16": "topk_small_kernel",
                  "qkv128": "topk_qkv_kernel"}.get(plan["kernel"], "topk_tile_kernel")
+        # arithmetic intensity 2*B*N*d / (N*d*elem) against the ridge (peak flops / HBM bytes):
+        # small batches are bound by the corpus stream
+        hbm_bound = flops / alg_bytes < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+        hbm_gbs = alg_bytes / (tile_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -275,11 +280,11 @@ def main() -> None:
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
             "roofline": {
                 "kernel": f"{kname} (fused MFMA Q.N^T + top-k, {plan['kernel']})",
-                "bound": "mfma",
-                "achieved": round(achieved_tf, 2),
-                "peak": peak,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tf / peak, 4),
+                "bound": "hbm" if hbm_bound else "mfma",
+                "achieved": round(hbm_gbs if hbm_bound else achieved_tf, 2),
+                "peak": HBM_PEAK_GBS if hbm_bound else peak,
+                "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                "frac": round(hbm_gbs / HBM_PEAK_GBS if hbm_bound else achieved_tf / peak, 4),
                 "traffic": read_traffic(kname, args.workload, B),
                 "algorithmic_flops_per_launch": flops,
                 "algorithmic_bytes_per_launch": alg_bytes,

@@ -210,7 +210,10 @@ def test_default_plans(cuda):
     ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
     ix.upsert(np.zeros((90000, 768), np.float32))
     assert ix.plan(1024, 10)["kernel"] == "tilelane128"
-    assert ix.plan(1, 16)["kernel"] == "tilelane128"
+    assert ix.plan(1, 16)["kernel"] == "small16"
+    assert ix.plan(16, 10)["kernel"] == "small16"
+    assert ix.plan(17, 10)["kernel"] == "tilelane128"
+    assert ix.plan(1, 17)["kernel"] == "tile128"
     assert ix.plan(2048, 10)["kernel"] == "qkv128"
     assert ix.plan(6144, 10)["kernel"] == "qkv128"
     assert ix.plan(1024, 17)["kernel"] == "tile128"
@@ -431,3 +434,94 @@ def test_t256_matches_tilelane(cuda, dtype, n, d, B, k, sample):
     b = [t.cpu().numpy() for t in ix.query(Q, k)]
     ix.close()
     _close_topk(a, b)
+
+
+# ---- small batches (B <= 16, bf16/f16, k <= 16): corpus-streaming 16x16x32 kernel -------------
+
+def test_small_plans(cuda):
+    from ah_rag.embeddings import DenseIndex
+    ix = DenseIndex(768, 5000, dtype="f32", device=cuda)  # fp32 keeps the exact single-chain kernels
+    ix.upsert(np.zeros((5000, 768), np.float32))
+    assert ix.plan(1, 10)["kernel"] != "small16"
+    ix.close()
+    ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
+    ix.upsert(np.zeros((90000, 768), np.float32))
+    p = ix.plan(1, 10)
+    assert p["kernel"] == "small16" and p["n_splits"] == 256
+    ix.set_debug_flags(32)  # an explicit kernel flag overrides the small-batch plan
+    assert ix.plan(1, 10)["kernel"] == "tilelane128"
+    ix.close()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n,d,B,k,norm", [
+    (90000, 768, 1, 10, False), (40001, 768, 16, 16, True), (33000, 384, 7, 5, False),
+    (300, 768, 1, 1, False), (17, 128, 3, 8, True), (1, 768, 2, 4, False), (5000, 100, 5, 12, True),
+    (5000, 102, 4, 10, True), (4000, 1100, 9, 10, False), (2000, 1000, 16, 16, True)])
+def test_small_matches_t256(cuda, dtype, n, d, B, k, norm):
+    """The small-batch kernel feeds the t256 kernel's 16x16x32 fragment map in the same k order,
+    and converts its queries with the convert kernel's arithmetic (in LDS; d = 102 and 1100 take
+    the converted query buffer instead): scores and rows bitwise equal to the t256 kernel; k > n
+    pads with (-inf, -1); splits that get fewer blocks than waves; ragged last block."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(500 + n + d + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d) * (3.0 if norm else 1.0)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    assert ix.plan(B, k)["kernel"] == "small16"
+    a = [t.cpu().numpy() for t in ix.query(Q, k, normalize=norm)]
+    ix.set_sample_rows(0)
+    ix.set_debug_flags(32768)
+    assert ix.plan(B, k)["kernel"] == "t256"
+    b = [t.cpu().numpy() for t in ix.query(Q, k, normalize=norm)]
+    ix.close()
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    kk = min(k, n)
+    if kk < k:
+        assert (a[1][:, kk:] == -1).all() and np.isneginf(a[0][:, kk:]).all()
+    # and against the f64 oracle on the rounded inputs
+    Qn = dr.normalize_rows(Q) if norm else Q
+    es, er = dr.topk(dr.round_to_storage(C, dtype), dr.round_to_storage(Qn, dtype), k, mode="f64")
+    assert np.abs(a[0][:, :kk] - es[:, :kk]).max() < 1e-4
+
+
+def test_small_ties_order_by_row(cuda):
+    """Duplicate rows score identically in bf16: the lowest row ids win across waves and splits."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(16)
+    base = _clustered(rng, 300, 768)
+    C = np.concatenate([base] * 40)  # 12000 rows, each vector 40 times
+    pick = rng.integers(0, 300, 16)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    assert ix.plan(16, 16)["kernel"] == "small16"
+    s, r = [t.cpu().numpy() for t in ix.query(base[pick], 16)]
+    ix.close()
+    np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(16)[None, :])
+    assert (s == s[:, :1]).all()
+
+
+def test_small_sharded_keys(cuda):
+    """row_base offsets and the key merge through the small-batch plan == one unsharded query."""
+    from ah_rag.embeddings import DenseIndex, merge_topk_keys
+    rng = np.random.default_rng(17)
+    C = _clustered(rng, 20000, 384)
+    Q = _clustered(rng, 5, 384)
+    full = DenseIndex(384, len(C), dtype="bf16", device=cuda)
+    full.upsert(C)
+    fs, fr = [t.cpu().numpy() for t in full.query(Q, 10)]
+    full.close()
+    bounds = [0, 7001, 13000, 20000]
+    lists = []
+    for g in range(3):
+        ix = DenseIndex(384, bounds[g + 1] - bounds[g], dtype="bf16", device=cuda)
+        ix.upsert(C[bounds[g]:bounds[g + 1]])
+        assert ix.plan(5, 10)["kernel"] == "small16"
+        lists.append(ix.query_keys(Q, 10, row_base=bounds[g]))
+        torch.cuda.synchronize()
+        ix.close()
+    s, r, _ = merge_topk_keys(torch.stack(lists, dim=1), 10)
+    np.testing.assert_array_equal(r.cpu().numpy(), fr)
+    np.testing.assert_array_equal(s.cpu().numpy(), fs)
