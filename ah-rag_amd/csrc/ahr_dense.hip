@@ -189,6 +189,7 @@ enum {
   kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
   kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
   kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
+  kFlagSmallWide = 65536,  // the small-batch kernel up to B = 64 (2 or 4 query groups; measured slower)
 };
 constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
@@ -2180,40 +2181,47 @@ __global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restric
 
 
 // =============================================================================================
-// topk_small_kernel (B <= 16, bf16/f16, k <= 16): every corpus row is read once and scored
-// against at most 16 queries, so the launch is bound by the corpus stream (HBM / MALL), not by
-// MFMA, and a 128-query tile wastes 7/8 of its work. No threshold pre-pass and no LDS staging
-// of the corpus: the (at most) 16 query rows are converted from fp32 straight into LDS by the
-// workgroup (convert_row_fast: the convert kernel's arithmetic, so the same rounded queries),
-// and each of the 16 waves streams 16-row corpus blocks straight into registers as the A
-// operand of v_mfma_f32_16x16x32 (lane l: row l & 15, 16-B chunk l / 16 of each 32-deep step,
-// the t256 kernel's fragment map, so the scores are bitwise those of its k-ordered chain).
+// topk_small_kernel (B <= 64, bf16/f16, k <= 16): every corpus row is read once and scored
+// against at most 64 queries, so the launch is bound by the corpus stream (HBM / MALL), not by
+// MFMA (intensity 2 B flop per corpus byte, below the ~315 flop/B ridge), and a 128-query tile
+// wastes most of its work. No threshold pre-pass and no LDS staging of the corpus: the query rows
+// are converted from fp32 straight into LDS by the workgroup (convert_row_fast: the convert
+// kernel's arithmetic, so the same rounded queries), and each wave streams 16-row corpus blocks
+// straight into registers as the A operand of v_mfma_f32_16x16x32 (lane l: row l & 15, 16-B chunk
+// l / 16 of each 32-deep step, the t256 kernel's fragment map, so the scores are bitwise those of
+// its k-ordered chain), one MFMA per 16-query group (NG = 1, 2, 4) per loaded fragment.
 // A wave's work is a sequence of (block, 8 k-steps) items in two register sets: the next item's
 // loads (the first one before the query staging) fly under the current item's MFMAs and the
-// block epilogue; 16 waves per CU keep up to 256 KiB of loads in flight. Epilogue: lane l holds query l & 15 at rows
-// 4 (l / 16) + i of the block and keeps a register list for it (the k-th key is its threshold);
-// at the end the 64 lists of each query (16 waves x 4 lane quarters) merge through LDS, one wave
-// per query, into one list per (query, split).
+// block epilogue; 16 (NG = 1) or 8 waves per CU keep 128-256 KiB of loads in flight.
+// Epilogue: lane l holds queries (l & 15) + 16 g at rows 4 (l / 16) + i of the block and keeps a
+// register list per query (its k-th key is the threshold); at the end the 4 W lists of each
+// query (W waves x 4 lane quarters) merge through LDS, one wave per query, into one list per
+// (query, split).
 // =============================================================================================
 namespace small {
-constexpr int kMaxQ = 16;
-constexpr int kWaves = 16;
-constexpr int kThreads = kWaves * 64;
-constexpr int kKC = 8;  // 32-deep k-steps per work item (one register set)
+constexpr int kMaxQ = 64;      // 4 groups of 16 queries
+constexpr int kKC = 8;         // 32-deep k-steps per work item (one register set)
 constexpr int kPitchPad = 16;  // query rows in LDS: pitch = row bytes + 16 (conflict-free reads)
-inline int lds_bytes(int64_t row_stride, int kcap) {
-  const int64_t q = kMaxQ * (row_stride + kPitchPad);
-  const int64_t l = (int64_t)kMaxQ * 4 * kWaves * kcap * 8;
+// waves per workgroup: 16 with one query group (<= 128 VGPRs), 8 with more (lists of NG queries
+// per lane, <= 256 VGPRs); one workgroup per CU either way
+__host__ __device__ constexpr int waves(int ng) { return ng == 1 ? 16 : 8; }
+inline int groups(int B) { return B <= 16 ? 1 : (B <= 32 ? 2 : 4); }
+// LDS: the NG * 16 query rows, later overlaid by one group's lane lists (16 x 4 W x KCAP keys)
+inline int lds_bytes(int64_t row_stride, int kcap, int ng) {
+  const int64_t q = (int64_t)16 * ng * (row_stride + kPitchPad);
+  const int64_t l = (int64_t)16 * 4 * waves(ng) * kcap * 8;
   return (int)(q > l ? q : l);
 }
 }  // namespace small
 
-template <int DT, int KCAP>
-__global__ __launch_bounds__(small::kThreads, 1) void topk_small_kernel(
+template <int DT, int KCAP, int NG>
+__global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
     const uint8_t* __restrict__ corpus, const float* __restrict__ qsrc, int dim, int normalize,
     const uint8_t* __restrict__ qconv, int64_t row_stride, int d_pad, int n_rows, int n_q, int n_steps,
     int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys) {
   static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
+  constexpr int W = small::waves(NG);
+  constexpr int kThreads = W * 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -2238,12 +2246,14 @@ __global__ __launch_bounds__(small::kThreads, 1) void topk_small_kernel(
   int cb = b_begin + wave, cs = 0;
   if (cb < b_end) load_item(A0, cb, 0);  // in flight while the queries are staged
 
-  // queries into LDS: converted from fp32 here (wave w: query w), or copied from the query buffer
+  // queries into LDS: converted from fp32 here (wave w: queries w, w + W, ...), or copied from
+  // the query buffer
   if (qsrc) {
-    if (wave < n_q) convert_row_fast(qsrc + (int64_t)wave * dim, dim, normalize, smem + wave * pitch, d_pad, DT, lane);
+    for (int r = wave; r < n_q; r += W)
+      convert_row_fast(qsrc + (int64_t)r * dim, dim, normalize, smem + r * pitch, d_pad, DT, lane);
   } else {
     const int chunks = (int)(row_stride >> 4);
-    for (int i = tid; i < n_q * chunks; i += small::kThreads) {
+    for (int i = tid; i < n_q * chunks; i += kThreads) {
       const int r = i / chunks;
       const int c = i - r * chunks;
       *reinterpret_cast<u32x4*>(smem + r * pitch + c * 16) =
@@ -2252,40 +2262,53 @@ __global__ __launch_bounds__(small::kThreads, 1) void topk_small_kernel(
   }
   __syncthreads();
 
-  uint64_t L[KCAP];
+  // lane: queries fr + 16 g (g < NG), rows 4 fq + i of each block
+  uint64_t L[NG][KCAP];
+  uint64_t thk[NG];  // the list's k-th key (0 while it holds fewer than k)
+  float thr[NG];
+  f32x4 acc[NG];
 #pragma unroll
-  for (int j = 0; j < KCAP; ++j) L[j] = 0;
-  uint64_t thk = 0;     // the list's k-th key (0 while it holds fewer than k)
-  float thr = -INFINITY;
-  const bool qok = fr < n_q;
+  for (int g = 0; g < NG; ++g) {
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[g][j] = 0;
+    thk[g] = 0;
+    thr[g] = fr + 16 * g < n_q ? -INFINITY : INFINITY;  // columns past n_q never pass
+    acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const unsigned char* qrow = smem + fr * pitch + fq * 16;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   // one item: issue the next item's loads into N, MFMAs over C, the block's epilogue after its
   // last item; returns false when the wave is done
   auto step = [&](u32x4 (&C)[small::kKC], u32x4 (&N)[small::kKC]) __attribute__((always_inline)) {
     int nb = cb, ns = cs + small::kKC;
     if (ns >= n_steps) {
       ns = 0;
-      nb += small::kWaves;
+      nb += W;
     }
     if (nb < b_end) load_item(N, nb, ns);
 #pragma unroll
     for (int j = 0; j < small::kKC; ++j)
-      if (cs + j < n_steps) mfma16(C[j], *reinterpret_cast<const u32x4*>(qrow + (cs + j) * 64), acc, DT);
+      if (cs + j < n_steps) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          mfma16(C[j], *reinterpret_cast<const u32x4*>(qrow + 16 * g * pitch + (cs + j) * 64), acc[g], DT);
+      }
     if (ns == 0) {
       const int r0 = cb * 16 + 4 * fq;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (qok && acc[i] >= thr && r0 + i < n_rows) {
-          const uint64_t key = make_key(acc[i], row_base + (uint32_t)(r0 + i));
-          if (key > thk) {
-            list_insert<KCAP>(L, key);
-            thk = list_at<KCAP>(L, k_out - 1);
-            thr = thk ? key_score(thk) : -INFINITY;
+      for (int g = 0; g < NG; ++g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (acc[g][i] >= thr[g] && r0 + i < n_rows) {
+            const uint64_t key = make_key(acc[g][i], row_base + (uint32_t)(r0 + i));
+            if (key > thk[g]) {
+              list_insert<KCAP>(L[g], key);
+              thk[g] = list_at<KCAP>(L[g], k_out - 1);
+              thr[g] = thk[g] ? key_score(thk[g]) : -INFINITY;
+            }
           }
         }
+        acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      acc = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     cb = nb;
     cs = ns;
@@ -2296,32 +2319,37 @@ __global__ __launch_bounds__(small::kThreads, 1) void topk_small_kernel(
     }
   }
 
-  // 64 lists per query -> LDS [query][wave * 4 + quarter][KCAP] -> one wave per query merges
-  __syncthreads();  // every wave is done reading the queries (the lists overlay them)
+  // per group: 4 W lists per query -> LDS [query][wave * 4 + quarter][KCAP] -> one wave per
+  // query merges them (k rounds of a DPP wave max) into one list per (query, split)
   uint64_t* lists = reinterpret_cast<uint64_t*>(smem);
-  if (qok) {
-    uint64_t* dst = lists + ((int64_t)fr * (4 * small::kWaves) + wave * 4 + fq) * KCAP;
 #pragma unroll
-    for (int j = 0; j < KCAP; ++j) dst[j] = L[j];
-  }
-  __syncthreads();
-  const int q = wave;
-  if (q < n_q) {
-    const uint64_t* src = lists + ((int64_t)q * (4 * small::kWaves) + lane) * KCAP;
-    uint64_t M[KCAP];
+  for (int g = 0; g < NG; ++g) {
+    if (16 * g >= n_q) break;  // uniform
+    __syncthreads();  // queries (g = 0) or the previous group's lists are no longer read
+    if (fr + 16 * g < n_q) {
+      uint64_t* dst = lists + ((int64_t)fr * (4 * W) + wave * 4 + fq) * KCAP;
 #pragma unroll
-    for (int j = 0; j < KCAP; ++j) M[j] = src[j];
-    uint64_t mine = 0;  // lane j keeps the j-th winner
-    for (int j = 0; j < k_out; ++j) {
-      const uint64_t best = wave_max_u64(M[0]);
-      if (best != 0 && M[0] == best) {
-#pragma unroll
-        for (int t = 0; t < KCAP - 1; ++t) M[t] = M[t + 1];
-        M[KCAP - 1] = 0;
-      }
-      if (lane == j) mine = best;
+      for (int j = 0; j < KCAP; ++j) dst[j] = L[g][j];
     }
-    if (lane < k_out) part_keys[((int64_t)q * n_splits + split) * k_out + lane] = mine;
+    __syncthreads();
+    for (int ql = wave; ql < 16; ql += W) {
+      const int q = 16 * g + ql;
+      if (q >= n_q) break;
+      uint64_t M[KCAP];
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) M[j] = lane < 4 * W ? lists[((int64_t)ql * (4 * W) + lane) * KCAP + j] : 0;
+      uint64_t mine = 0;  // lane j keeps the j-th winner
+      for (int j = 0; j < k_out; ++j) {
+        const uint64_t best = wave_max_u64(M[0]);
+        if (best != 0 && M[0] == best) {
+#pragma unroll
+          for (int t = 0; t < KCAP - 1; ++t) M[t] = M[t + 1];
+          M[KCAP - 1] = 0;
+        }
+        if (lane == j) mine = best;
+      }
+      if (lane < k_out) part_keys[((int64_t)q * n_splits + split) * k_out + lane] = mine;
+    }
   }
 }
 
@@ -2470,7 +2498,7 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 // ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
 // 3 = 128x128 lane-local tile kernel, 5 = query-resident kernel (dimension halves over wave pairs);
 // 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed), 6 = 256x256 16x16x32
-// kernel (opt-in), 7 = small-batch streaming kernel (B <= 16)
+// kernel (opt-in), 7 = small-batch streaming kernel (B <= 16; <= 64 opt-in)
 enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
        KERNEL_T256 = 6, KERNEL_SMALL = 7 };
 
@@ -2508,23 +2536,28 @@ bool qkv_ok(const ahr_index* ix, int B, int k) {
   return B >= 2048 && B <= 8192 && ix->sample_rows > 0 && ix->count <= 32 * (int64_t)ix->sample_rows;
 }
 
-// The small-batch streaming kernel: B <= 16, bf16/f16, k <= 16, the 16 query rows (or the
-// 64 x KCAP lists per query of the end merge) within LDS; not under an explicit kernel flag.
+// The small-batch streaming kernel: B <= 16 (<= 64 under kFlagSmallWide), bf16/f16, k <= 16, the
+// query rows (or one group's lane lists of the end merge) within LDS; not under a kernel flag.
 bool small_ok(const ahr_index* ix, int B, int k) {
   if (B > small::kMaxQ || k > 16 || ix->dtype == AHR_F32) return false;
+  // 2 and 4 query groups: the per-lane list inserts (nearly every score of a lane's short stream)
+  // outweigh the saved pre-pass (hotpot90k: 51 us at B = 32, 81 us at B = 64, vs the 128x128
+  // lane-local kernel's ~40 us with its pre-pass), so only under the ablation flag
+  if (B > 16 && !(ix->debug_flags & kFlagSmallWide)) return false;
   if (ix->debug_flags & kKernelFlags) return false;
-  return small::lds_bytes(ix->row_stride, 16) <= 160 * 1024;
+  return small::lds_bytes(ix->row_stride, 16, small::groups(B)) <= 160 * 1024;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
   if (small_ok(ix, B, k)) {
-    // one workgroup (16 waves) per CU, at least one 16-row block per wave
+    // one workgroup per CU, at least one 16-row block per wave
     p.kernel = KERNEL_SMALL;
     p.qblocks = 1;
     p.n_row_tiles = (int)cdiv(ix->count, 16);
-    p.n_splits = (int)std::max<int64_t>(1, std::min<int64_t>(256, cdiv(p.n_row_tiles, small::kWaves)));
+    p.n_splits = (int)std::max<int64_t>(
+        1, std::min<int64_t>(256, cdiv(p.n_row_tiles, small::waves(small::groups(B)))));
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     p.xcd_remap = false;
     return p;
@@ -2756,20 +2789,31 @@ void launch_lane_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, 
     launch_lane<DT, 16, NB, BJ, WR, WQ, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
 }
 
-template <int DT, int KCAP>
+template <int DT, int KCAP, int NG>
 void launch_small(const ahr_index* ix, const SearchPlan& p, const float* q, int normalize_q, int B, int k,
                   uint32_t row_base, hipStream_t s) {
-  constexpr auto kern = &topk_small_kernel<DT, KCAP>;
-  const int lds = small::lds_bytes(ix->row_stride, KCAP);
+  constexpr auto kern = &topk_small_kernel<DT, KCAP, NG>;
+  const int lds = small::lds_bytes(ix->row_stride, KCAP, NG);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::kThreads), lds, s, ix->rows, q, ix->dim,
+  hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::waves(NG) * 64), lds, s, ix->rows, q, ix->dim,
                      normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, (int)ix->count, B,
                      (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part);
+}
+
+template <int DT, int NG>
+void launch_small_k(const ahr_index* ix, const SearchPlan& p, const float* q, int normalize_q, int B, int k,
+                    uint32_t row_base, hipStream_t s) {
+  if (k <= 8)
+    launch_small<DT, 8, NG>(ix, p, q, normalize_q, B, k, row_base, s);
+  else if (k <= 12)
+    launch_small<DT, 12, NG>(ix, p, q, normalize_q, B, k, row_base, s);
+  else
+    launch_small<DT, 16, NG>(ix, p, q, normalize_q, B, k, row_base, s);
 }
 
 // queries converted inside topk_small_kernel (convert_row_fast's shape) instead of by the convert kernel
@@ -2784,12 +2828,11 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     if (p.kernel == KERNEL_SMALL) {
       prof_mark(ix, 2, s);
       const float* qs = small_fuses_convert(ix) ? q : nullptr;
-      if (k <= 8)
-        launch_small<DT, 8>(ix, p, qs, normalize_q, B, k, row_base, s);
-      else if (k <= 12)
-        launch_small<DT, 12>(ix, p, qs, normalize_q, B, k, row_base, s);
-      else
-        launch_small<DT, 16>(ix, p, qs, normalize_q, B, k, row_base, s);
+      switch (small::groups(B)) {
+        case 1: launch_small_k<DT, 1>(ix, p, qs, normalize_q, B, k, row_base, s); break;
+        case 2: launch_small_k<DT, 2>(ix, p, qs, normalize_q, B, k, row_base, s); break;
+        default: launch_small_k<DT, 4>(ix, p, qs, normalize_q, B, k, row_base, s); break;
+      }
       return;
     }
   }
@@ -3166,7 +3209,7 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
-                             kKernelFlags);
+                             kKernelFlags | kFlagSmallWide);
   return AHR_OK;
 }
 

@@ -105,7 +105,9 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
 /* Ablation switches for profiling, never set in production. Correct results: 8 = always the
  * 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile kernel at any
- * batch (k <= 16), 64 = the 256x128 lane kernel (k <= 16). Garbage results (cost splits):
+ * batch (k <= 16), 64 = the 256x128 lane kernel (k <= 16), 2048 = no query-resident kernel,
+ * 4096 = the query-resident kernel wherever it applies, 32768 = the 256x256 16x16x32 kernel,
+ * 65536 = the small-batch streaming kernel up to B = 64. Garbage results (cost splits):
  * 2 = skip the top-k epilogue, 256 = lane epilogue stops after the group maxima, 512 = tile
  * kernel (cooperative) loads operands for its first tile only. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
@@ -113,7 +115,8 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
  * *kernel: 0 = 128x128 tile kernel (cooperative screening; k > 16), 1 = 256x256 lane kernel
  * (k <= 16, B >= 6144), 2 = 256x128 lane kernel, 3 = 128x128 lane-local tile kernel (k <= 16,
- * B < 6144). */
+ * B < 6144), 5 = query-resident kernel (bf16/f16, 2048 <= B <= 8192), 6 = 256x256 16x16x32
+ * kernel (opt-in), 7 = small-batch streaming kernel (bf16/f16, B <= 16, k <= 16). */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 

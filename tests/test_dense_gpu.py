@@ -210,8 +210,8 @@ def test_default_plans(cuda):
     ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
     ix.upsert(np.zeros((90000, 768), np.float32))
     assert ix.plan(1024, 10)["kernel"] == "tilelane128"
-    assert ix.plan(1, 16)["kernel"] == "small16"
-    assert ix.plan(16, 10)["kernel"] == "small16"
+    assert ix.plan(1, 16)["kernel"] == "small"
+    assert ix.plan(16, 10)["kernel"] == "small"
     assert ix.plan(17, 10)["kernel"] == "tilelane128"
     assert ix.plan(1, 17)["kernel"] == "tile128"
     assert ix.plan(2048, 10)["kernel"] == "qkv128"
@@ -436,20 +436,23 @@ def test_t256_matches_tilelane(cuda, dtype, n, d, B, k, sample):
     _close_topk(a, b)
 
 
-# ---- small batches (B <= 16, bf16/f16, k <= 16): corpus-streaming 16x16x32 kernel -------------
+# ---- small batches (B <= 16; <= 64 opt-in, bf16/f16, k <= 16): corpus-streaming 16x16x32 kernel -------------
 
 def test_small_plans(cuda):
     from ah_rag.embeddings import DenseIndex
     ix = DenseIndex(768, 5000, dtype="f32", device=cuda)  # fp32 keeps the exact single-chain kernels
     ix.upsert(np.zeros((5000, 768), np.float32))
-    assert ix.plan(1, 10)["kernel"] != "small16"
+    assert ix.plan(1, 10)["kernel"] != "small"
     ix.close()
     ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
     ix.upsert(np.zeros((90000, 768), np.float32))
     p = ix.plan(1, 10)
-    assert p["kernel"] == "small16" and p["n_splits"] == 256
+    assert p["kernel"] == "small" and p["n_splits"] == 256
     ix.set_debug_flags(32)  # an explicit kernel flag overrides the small-batch plan
     assert ix.plan(1, 10)["kernel"] == "tilelane128"
+    ix.set_debug_flags(65536)  # 2 and 4 query groups (opt-in)
+    assert ix.plan(64, 10)["kernel"] == "small"
+    assert ix.plan(65, 10)["kernel"] == "tilelane128"
     ix.close()
 
 
@@ -457,19 +460,24 @@ def test_small_plans(cuda):
 @pytest.mark.parametrize("n,d,B,k,norm", [
     (90000, 768, 1, 10, False), (40001, 768, 16, 16, True), (33000, 384, 7, 5, False),
     (300, 768, 1, 1, False), (17, 128, 3, 8, True), (1, 768, 2, 4, False), (5000, 100, 5, 12, True),
-    (5000, 102, 4, 10, True), (4000, 1100, 9, 10, False), (2000, 1000, 16, 16, True)])
+    (5000, 102, 4, 10, True), (4000, 1100, 9, 10, False), (2000, 1000, 16, 16, True),
+    (40001, 768, 64, 10, True), (33000, 384, 33, 16, False), (5000, 102, 20, 10, True),
+    (4000, 1100, 40, 10, False), (2000, 1000, 50, 5, True), (300, 768, 17, 1, False), (90000, 768, 32, 10, False)])
 def test_small_matches_t256(cuda, dtype, n, d, B, k, norm):
     """The small-batch kernel feeds the t256 kernel's 16x16x32 fragment map in the same k order,
     and converts its queries with the convert kernel's arithmetic (in LDS; d = 102 and 1100 take
     the converted query buffer instead): scores and rows bitwise equal to the t256 kernel; k > n
-    pads with (-inf, -1); splits that get fewer blocks than waves; ragged last block."""
+    pads with (-inf, -1); splits that get fewer blocks than waves; ragged last block; 1, 2 and 4
+    groups of 16 queries (B <= 16, 32, 64; 2 and 4 under flag 65536) with ragged last groups."""
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(500 + n + d + B + k)
     C = _clustered(rng, n, d)
     Q = _clustered(rng, B, d) * (3.0 if norm else 1.0)
     ix = DenseIndex(d, n, dtype=dtype, device=cuda)
     ix.upsert(C)
-    assert ix.plan(B, k)["kernel"] == "small16"
+    if B > 16:
+        ix.set_debug_flags(65536)
+    assert ix.plan(B, k)["kernel"] == "small"
     a = [t.cpu().numpy() for t in ix.query(Q, k, normalize=norm)]
     ix.set_sample_rows(0)
     ix.set_debug_flags(32768)
@@ -496,7 +504,7 @@ def test_small_ties_order_by_row(cuda):
     pick = rng.integers(0, 300, 16)
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
-    assert ix.plan(16, 16)["kernel"] == "small16"
+    assert ix.plan(16, 16)["kernel"] == "small"
     s, r = [t.cpu().numpy() for t in ix.query(base[pick], 16)]
     ix.close()
     np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(16)[None, :])
@@ -518,7 +526,7 @@ def test_small_sharded_keys(cuda):
     for g in range(3):
         ix = DenseIndex(384, bounds[g + 1] - bounds[g], dtype="bf16", device=cuda)
         ix.upsert(C[bounds[g]:bounds[g + 1]])
-        assert ix.plan(5, 10)["kernel"] == "small16"
+        assert ix.plan(5, 10)["kernel"] == "small"
         lists.append(ix.query_keys(Q, 10, row_base=bounds[g]))
         torch.cuda.synchronize()
         ix.close()
