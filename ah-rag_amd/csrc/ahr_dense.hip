@@ -2192,19 +2192,27 @@ __global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restric
 // its k-ordered chain), one MFMA per 16-query group (NG = 1, 2, 4) per loaded fragment.
 // A wave's work is a sequence of (block, 8 k-steps) items in two register sets: the next item's
 // loads (the first one before the query staging) fly under the current item's MFMAs and the
-// block epilogue; 16 (NG = 1) or 8 waves per CU keep 128-256 KiB of loads in flight.
+// block epilogue; 8 waves per workgroup keep 128 KiB of loads in flight, and two workgroups
+// (two batches in flight) fit on a CU.
 // Epilogue: lane l holds queries (l & 15) + 16 g at rows 4 (l / 16) + i of the block and keeps a
 // register list per query (its k-th key is the threshold); at the end the 4 W lists of each
 // query (W waves x 4 lane quarters) merge through LDS, one wave per query, into one list per
 // (query, split).
 // =============================================================================================
+#ifndef AHR_SMALL_WAVES
+#define AHR_SMALL_WAVES 8  // waves per workgroup with one query group (A/B builds override)
+#endif
+#ifndef AHR_SMALL_KC
+#define AHR_SMALL_KC 8
+#endif
 namespace small {
 constexpr int kMaxQ = 64;      // 4 groups of 16 queries
-constexpr int kKC = 8;         // 32-deep k-steps per work item (one register set)
+constexpr int kKC = AHR_SMALL_KC;  // 32-deep k-steps per work item (one register set)
 constexpr int kPitchPad = 16;  // query rows in LDS: pitch = row bytes + 16 (conflict-free reads)
-// waves per workgroup: 16 with one query group (<= 128 VGPRs), 8 with more (lists of NG queries
-// per lane, <= 256 VGPRs); one workgroup per CU either way
-__host__ __device__ constexpr int waves(int ng) { return ng == 1 ? 16 : 8; }
+// waves per workgroup: 8 (A/B at B = 1 / 16, two batches in flight: 45.1 k / 594 k queries/s
+// with 8 waves, 42.9 k / 516 k with 12, 38.2 k / 471 k with 16 — a 16-wave workgroup fills a CU's
+// VGPRs, so the other batch's kernel cannot co-reside; serial latency 8 % higher with 8)
+__host__ __device__ constexpr int waves(int ng) { return ng == 1 ? AHR_SMALL_WAVES : 8; }
 inline int groups(int B) { return B <= 16 ? 1 : (B <= 32 ? 2 : 4); }
 // LDS: the NG * 16 query rows, later overlaid by one group's lane lists (16 x 4 W x KCAP keys)
 inline int lds_bytes(int64_t row_stride, int kcap, int ng) {

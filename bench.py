@@ -18,6 +18,7 @@ The data is synthetic (no dataset or encoder weights offline).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -100,15 +101,20 @@ def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float)
 def read_traffic(kernel: str, workload: str, batch: int):
     """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), if it was
     measured on this workload and batch (else None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            data = json.load(f)
+    paths = [os.path.join(ROOT, "profiles", "pmc_traffic.json")]
+    paths += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*", "pmc_traffic.json")))
+    for path in paths:
+        try:
+            with open(path) as f:
+                data = json.load(f)
+        except Exception:
+            continue
         if data.get("_workload", "hotpot90k") != workload or data.get("_batch", 1024) != batch:
-            return None
-        return data.get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+            continue
+        v = data.get(kernel, {}).get("hbm_bytes_per_launch")
+        if v is not None:
+            return v
+    return None
 
 
 def main() -> None:
