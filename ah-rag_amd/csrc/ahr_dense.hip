@@ -2361,6 +2361,151 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   }
 }
 
+// topk_small_f32_kernel (fp32 exact mode, B <= 4, k <= 16): the small-batch stream for the
+// drop-in search's fp32 index. The exact-mode contract is one fmaf chain per (row, query) in
+// increasing k, so one lane owns one corpus row of a 64-row item and runs the chain on the VALU
+// (B <= 4 queries: <= 4 fmas per loaded float, far below the stream's cost); the stored (evens |
+// odds) permutation of each group of 8 is undone by the order of the fmas. Loads: one 128-B line
+// per lane per step in two register sets (the next step's line in flight under the current
+// fmas). Queries (the convert kernel's permuted fp32 rows) are broadcast reads from LDS. Each
+// lane keeps a register list per query; at the end every wave reduces its 64 lane lists (k rounds
+// of a DPP wave max) and one wave merges the 8 wave lists through LDS into one list per
+// (query, split).
+namespace smallf32 {
+constexpr int kWaves = 8;
+constexpr int kMaxQ = 4;
+}  // namespace smallf32
+
+template <int KCAP, int NQ>
+__global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kernel(
+    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qconv, int64_t row_stride, int n_rows, int n_q,
+    int n_lines, int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys) {
+  constexpr int W = smallf32::kWaves;
+  __shared__ __attribute__((aligned(16))) float qs[NQ * 1024];  // d_pad <= 1024
+  __shared__ uint64_t wl[NQ][W][KCAP];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int split = blockIdx.x;
+  const int n_items = (n_rows + 63) >> 6;
+  const int i_begin = (int)((int64_t)split * n_items / n_splits);
+  const int i_end = (int)((int64_t)(split + 1) * n_items / n_splits);
+  const int d_pad = (int)(row_stride >> 2);
+
+  u32x4 A0[8], A1[8];
+  int ci = i_begin + wave, cl = 0;  // current item, current 128-B line of the row
+  auto load_line = [&](u32x4 (&A)[8], int item, int line) __attribute__((always_inline)) {
+    const int row = item * 64 + lane;
+    const u32x4* src = reinterpret_cast<const u32x4*>(corpus + (int64_t)row * row_stride + line * 128);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) A[j] = src[j];
+  };
+  if (ci < i_end) load_line(A0, ci, 0);
+  for (int i = tid; i < n_q * d_pad / 4; i += W * 64) {
+    const int r = i / (d_pad / 4);
+    const int c = i - r * (d_pad / 4);
+    reinterpret_cast<f32x4*>(qs)[r * 256 + c] = *reinterpret_cast<const f32x4*>(qconv + (int64_t)r * row_stride + c * 16);
+  }
+  __syncthreads();
+
+  uint64_t L[NQ][KCAP];
+  uint64_t thk[NQ];
+  float acc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[q][j] = 0;
+    thk[q] = 0;
+    acc[q] = 0.f;
+  }
+  auto step = [&](u32x4 (&C)[8], u32x4 (&N)[8]) __attribute__((always_inline)) {
+    int ni = ci, nl = cl + 1;
+    if (nl >= n_lines) {
+      nl = 0;
+      ni += W;
+    }
+    if (ni < i_end) load_line(N, ni, nl);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // 4 groups of 8 per line
+      const f32x4 lo = __builtin_bit_cast(f32x4, C[2 * g]);
+      const f32x4 hi = __builtin_bit_cast(f32x4, C[2 * g + 1]);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if (q < n_q) {
+          const float* qp = qs + q * 1024 + cl * 32 + g * 8;
+          const f32x4 qlo = *reinterpret_cast<const f32x4*>(qp);
+          const f32x4 qhi = *reinterpret_cast<const f32x4*>(qp + 4);
+          // logical k order 8g + 0..7 = stored positions 0, 4, 1, 5, 2, 6, 3, 7
+          float a = acc[q];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            a = fmaf(lo[m], qlo[m], a);
+            a = fmaf(hi[m], qhi[m], a);
+          }
+          acc[q] = a;
+        }
+      }
+    }
+    if (nl == 0) {
+      const int row = ci * 64 + lane;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if (q < n_q && row < n_rows) {
+          const uint64_t key = make_key(acc[q], row_base + (uint32_t)row);
+          if (key > thk[q]) {
+            list_insert<KCAP>(L[q], key);
+            thk[q] = list_at<KCAP>(L[q], k_out - 1);
+          }
+        }
+        acc[q] = 0.f;
+      }
+    }
+    ci = ni;
+    cl = nl;
+    return ci < i_end;
+  };
+  if (ci < i_end) {
+    while (step(A0, A1) && step(A1, A0)) {
+    }
+  }
+  // per query: the wave's 64 lane lists -> one list (k rounds of a wave max) -> LDS; wave 0
+  // merges the W wave lists
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (q >= n_q) break;
+    uint64_t mine = 0;
+    for (int j = 0; j < k_out; ++j) {
+      const uint64_t best = wave_max_u64(L[q][0]);
+      if (best != 0 && L[q][0] == best) {
+#pragma unroll
+        for (int t = 0; t < KCAP - 1; ++t) L[q][t] = L[q][t + 1];
+        L[q][KCAP - 1] = 0;
+      }
+      if (lane == j) mine = best;
+    }
+    if (lane < KCAP) wl[q][wave][lane] = lane < k_out ? mine : 0;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    for (int q = 0; q < n_q; ++q) {
+      uint64_t M[KCAP];
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) M[j] = lane < W ? wl[q][lane][j] : 0;
+      uint64_t mine = 0;
+      for (int j = 0; j < k_out; ++j) {
+        const uint64_t best = wave_max_u64(M[0]);
+        if (best != 0 && M[0] == best) {
+#pragma unroll
+          for (int t = 0; t < KCAP - 1; ++t) M[t] = M[t + 1];
+          M[KCAP - 1] = 0;
+        }
+        if (lane == j) mine = best;
+      }
+      if (lane < k_out) part_keys[((int64_t)q * n_splits + split) * k_out + lane] = mine;
+    }
+  }
+}
+
 // k-way merge of up to 512 sorted lists per query (n_lists * k_in <= 8192), one 256-thread
 // workgroup per query: every key comes into LDS with coalesced loads in one go (a head-advancing
 // merge over global memory pays one dependent L2 latency per output), then k rounds of a
@@ -2547,7 +2692,9 @@ bool qkv_ok(const ahr_index* ix, int B, int k) {
 // The small-batch streaming kernel: B <= 16 (<= 64 under kFlagSmallWide), bf16/f16, k <= 16, the
 // query rows (or one group's lane lists of the end merge) within LDS; not under a kernel flag.
 bool small_ok(const ahr_index* ix, int B, int k) {
-  if (B > small::kMaxQ || k > 16 || ix->dtype == AHR_F32) return false;
+  if (ix->dtype == AHR_F32)  // exact mode: the VALU fma-chain stream (topk_small_f32_kernel)
+    return B <= smallf32::kMaxQ && k <= 16 && ix->d_pad <= 1024 && !(ix->debug_flags & kKernelFlags);
+  if (B > small::kMaxQ || k > 16) return false;
   // 2 and 4 query groups: the per-lane list inserts (nearly every score of a lane's short stream)
   // outweigh the saved pre-pass (hotpot90k: 51 us at B = 32, 81 us at B = 64, vs the 128x128
   // lane-local kernel's ~40 us with its pre-pass), so only under the ablation flag
@@ -2563,9 +2710,10 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     // one workgroup per CU, at least one 16-row block per wave
     p.kernel = KERNEL_SMALL;
     p.qblocks = 1;
-    p.n_row_tiles = (int)cdiv(ix->count, 16);
+    const bool f32 = ix->dtype == AHR_F32;  // 64-row items (a row per lane) vs 16-row blocks
+    p.n_row_tiles = (int)cdiv(ix->count, f32 ? 64 : 16);
     p.n_splits = (int)std::max<int64_t>(
-        1, std::min<int64_t>(256, cdiv(p.n_row_tiles, small::waves(small::groups(B)))));
+        1, std::min<int64_t>(256, cdiv(p.n_row_tiles, f32 ? smallf32::kWaves : small::waves(small::groups(B)))));
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     p.xcd_remap = false;
     return p;
@@ -2825,14 +2973,38 @@ void launch_small_k(const ahr_index* ix, const SearchPlan& p, const float* q, in
 }
 
 // queries converted inside topk_small_kernel (convert_row_fast's shape) instead of by the convert kernel
-inline bool small_fuses_convert(const ahr_index* ix) { return (ix->dim & 3) == 0 && ix->d_pad <= 1024; }
+inline bool small_fuses_convert(const ahr_index* ix) {
+  return ix->dtype != AHR_F32 && (ix->dim & 3) == 0 && ix->d_pad <= 1024;
+}
+
+template <int KCAP>
+void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, hipStream_t s) {
+  const int n_lines = (int)(ix->row_stride / 128);
+  if (B == 1)
+    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 1>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), 0, s,
+                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part);
+  else
+    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 4>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), 0, s,
+                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part);
+}
 
 template <int DT>
 void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const float* q,
                    int normalize_q, hipStream_t s) {
   const float* thr = nullptr;
   prof_mark(ix, 1, s);
-  if constexpr (DT != DT_F32) {
+  if constexpr (DT == DT_F32) {
+    if (p.kernel == KERNEL_SMALL) {
+      prof_mark(ix, 2, s);
+      if (k <= 8)
+        launch_small_f32_k<8>(ix, p, B, k, row_base, s);
+      else if (k <= 12)
+        launch_small_f32_k<12>(ix, p, B, k, row_base, s);
+      else
+        launch_small_f32_k<16>(ix, p, B, k, row_base, s);
+      return;
+    }
+  } else {
     if (p.kernel == KERNEL_SMALL) {
       prof_mark(ix, 2, s);
       const float* qs = small_fuses_convert(ix) ? q : nullptr;

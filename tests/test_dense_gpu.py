@@ -440,8 +440,14 @@ def test_t256_matches_tilelane(cuda, dtype, n, d, B, k, sample):
 
 def test_small_plans(cuda):
     from ah_rag.embeddings import DenseIndex
-    ix = DenseIndex(768, 5000, dtype="f32", device=cuda)  # fp32 keeps the exact single-chain kernels
+    ix = DenseIndex(768, 5000, dtype="f32", device=cuda)  # fp32: the VALU fma-chain stream, B <= 4
     ix.upsert(np.zeros((5000, 768), np.float32))
+    assert ix.plan(1, 10)["kernel"] == "small"
+    assert ix.plan(4, 16)["kernel"] == "small"
+    assert ix.plan(5, 10)["kernel"] != "small"
+    assert ix.plan(1, 17)["kernel"] != "small"
+    ix.close()
+    ix = DenseIndex(1100, 100, dtype="f32", device=cuda)  # d_pad > 1024: the tile path
     assert ix.plan(1, 10)["kernel"] != "small"
     ix.close()
     ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
@@ -533,3 +539,33 @@ def test_small_sharded_keys(cuda):
     s, r, _ = merge_topk_keys(torch.stack(lists, dim=1), 10)
     np.testing.assert_array_equal(r.cpu().numpy(), fr)
     np.testing.assert_array_equal(s.cpu().numpy(), fs)
+
+
+@pytest.mark.parametrize("n,d,B,k,norm", [
+    (90000, 768, 1, 10, False), (40001, 768, 4, 16, True), (33000, 384, 3, 5, False), (1, 768, 1, 4, False),
+    (300, 100, 2, 1, True), (65, 1000, 4, 12, False), (5000, 102, 1, 8, True)])
+def test_small_f32_bit_exact(cuda, n, d, B, k, norm):
+    """fp32 small batches (B <= 4): one lane runs each (row, query) fma chain in k order on the
+    VALU, undoing the stored lane permutation: rows and scores bit-identical to the oracle; ragged
+    64-row items, k > n, normalisation in the convert kernel."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(900 + n + d + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d) * (2.0 if norm else 1.0)
+    ix = DenseIndex(d, n, dtype="f32", device=cuda)
+    ix.upsert(C)
+    assert ix.plan(B, k)["kernel"] == "small"
+    s, r = [t.cpu().numpy() for t in ix.query(Q, k, normalize=norm)]
+    ix.close()
+    Qn = Q
+    if norm:  # the device normalisation (fp32 wave reduction) is the convert kernel's, as in the tile path
+        ix2 = DenseIndex(d, max(1, B), dtype="f32", device=cuda)
+        ix2.upsert(Q, normalize=True)
+        Qn = ix2.read(0, B).cpu().numpy()
+        ix2.close()
+    es, er = dr.topk(C, Qn, k, mode="fma")
+    kk = min(k, n)
+    np.testing.assert_array_equal(r[:, :kk], er[:, :kk])
+    np.testing.assert_array_equal(s[:, :kk].astype(np.float32), es[:, :kk].astype(np.float32))
+    if kk < k:
+        assert (r[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
