@@ -254,7 +254,7 @@ def main() -> None:
         plan = local.plan(B, k)
         kname = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
                  "tilelane128": "topk_tilelane_kernel", "t256": "topk_t256_kernel",
-                 "small": "topk_small_kernel",
+                 "small": "topk_small_f32_kernel" if dtype == "f32" else "topk_small_kernel",
                  "qkv128": "topk_qkv_kernel"}.get(plan["kernel"], "topk_tile_kernel")
         # arithmetic intensity 2*B*N*d / (N*d*elem) against the ridge (peak flops / HBM bytes):
         # small batches are bound by the corpus stream

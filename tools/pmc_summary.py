@@ -70,7 +70,7 @@ def main() -> None:
     for k in sorted(set(fetch) | set(write) | set(dur)):
         base = k.split("<")[0]
         if base not in ("topk_tile_kernel", "topk_tilelane_kernel", "topk_lane_kernel", "topk_qkv_kernel", "topk_t256_kernel",
-                        "topk_small_kernel", "merge_block_kernel", "merge_lane_lists_kernel", "merge_heads_kernel",
+                        "topk_small_kernel", "topk_small_f32_kernel", "merge_block_kernel", "merge_lane_lists_kernel", "merge_heads_kernel",
                         "merge_kernel", "sample_kth_kernel", "convert_rows_kernel", "expand_rerank_kernel",
                         "expand_kernel"):
             continue
