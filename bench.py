@@ -285,7 +285,7 @@ def main() -> None:
             },
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
             "roofline": {
-                "kernel": f"{kname} (fused MFMA Q.N^T + top-k, {plan['kernel']})",
+                "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} Q.N^T + top-k, {plan['kernel']})",
                 "bound": "hbm" if hbm_bound else "mfma",
                 "achieved": round(hbm_gbs if hbm_bound else achieved_tf, 2),
                 "peak": HBM_PEAK_GBS if hbm_bound else peak,
