@@ -2508,8 +2508,9 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
 
 // k-way merge of up to 512 sorted lists per query (n_lists * k_in <= 8192), one 256-thread
 // workgroup per query: every key comes into LDS with coalesced loads in one go (a head-advancing
-// merge over global memory pays one dependent L2 latency per output), then k rounds of a
-// block-wide max over the list heads (thread t owns lists t and t + 256).
+// merge over global memory pays one dependent L2 latency per output), then one wave takes k
+// rounds of a DPP wave max over the list heads held in registers (lane l owns lists l + 64 u),
+// advancing a head with an LDS read: no barrier per output.
 constexpr int kMergeBlockKeys = 8192;
 __global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __restrict__ in, int n_lists, int k_in,
                                                           int k, float* __restrict__ scores,
@@ -2536,35 +2537,43 @@ __global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __rest
     const int i = tid + 256 * u;
     if (i < n) kb[i] = v[u];
   }
-  uint64_t* wmax = kb + n;  // [2 round parities][4 waves]
   __syncthreads();
-  const int l0 = tid, l1 = tid + 256;
-  int p0 = 0, p1 = 0;
-  uint64_t h0 = (l0 < n_lists && k_in > 0) ? kb[l0 * k_in] : 0;
-  uint64_t h1 = (l1 < n_lists && k_in > 0) ? kb[l1 * k_in] : 0;
-  for (int j = 0; j < k; ++j) {
-    const uint64_t wm = wave_max_u64(h0 > h1 ? h0 : h1);
-    // parity slots: a wave writing round j + 2 has passed round j + 1's barrier, which every
-    // wave reaches only after reading round j
-    if (lane == 0) wmax[(j & 1) * 4 + wave] = wm;
-    __syncthreads();
-    uint64_t best = wmax[(j & 1) * 4];
+  if (wave != 0) return;
+  // one wave walks the heads (lane l owns lists l + 64 u): no barrier per output
+  constexpr int kH = 8;  // n_lists <= 512
+  int ptr[kH];
+  uint64_t head[kH];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) best = max_u64(best, wmax[(j & 1) * 4 + w]);
-    if (best != 0) {
-      if (h0 == best) {
-        ++p0;
-        h0 = p0 < k_in ? kb[l0 * k_in + p0] : 0;
-      } else if (h1 == best) {
-        ++p1;
-        h1 = p1 < k_in ? kb[l1 * k_in + p1] : 0;
+  for (int u = 0; u < kH; ++u) {
+    const int l = lane + 64 * u;
+    ptr[u] = 0;
+    head[u] = (l < n_lists && k_in > 0) ? kb[l * k_in] : 0;
+  }
+  uint64_t mine = 0;  // lane j keeps the j-th winner (k <= 64 here)
+  for (int j = 0; j < k; ++j) {
+    uint64_t m = head[0];
+#pragma unroll
+    for (int u = 1; u < kH; ++u) m = max_u64(m, head[u]);
+    const uint64_t best = wave_max_u64(m);
+    if (best != 0 && m == best) {
+#pragma unroll
+      for (int u = 0; u < kH; ++u) {
+        if (head[u] == best) {
+          const int l = lane + 64 * u;
+          ++ptr[u];
+          head[u] = ptr[u] < k_in ? kb[l * k_in + ptr[u]] : 0;
+        }
       }
     }
-    if (tid == 0) {
-      const int64_t o = (int64_t)q * k + j;
-      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
-      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
-      if (keys_out) keys_out[o] = best;
+    if (lane == (j & 63)) mine = best;
+    if ((j & 63) == 63 || j == k - 1) {  // flush a full (or the last) window of 64 outputs
+      const int j0 = j & ~63;
+      if (j0 + lane <= j) {
+        const int64_t o = (int64_t)q * k + j0 + lane;
+        if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
+        if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
+        if (keys_out) keys_out[o] = mine;
+      }
     }
   }
 }
