@@ -253,6 +253,7 @@ class DenseIndex:
             rows = torch.empty((B, k), dtype=torch.int32, device=self.device)
         else:
             scores, rows = out
+        _on_stream(stream, self.device, q, scores, rows)
         with torch.cuda.device(self.device):
             nat.check(nat.lib().ahr_index_query(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
                                                 nat.ptr(scores), nat.ptr(rows), nat.stream_ptr(stream)),
@@ -266,11 +267,27 @@ class DenseIndex:
         q = _as_f32_device(queries, self.device)
         B = q.shape[0]
         keys = out if out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
+        _on_stream(stream, self.device, q, keys)
         with torch.cuda.device(self.device):
             nat.check(nat.lib().ahr_index_query_keys(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
                                                      int(row_base), nat.ptr(keys), nat.stream_ptr(stream)),
                       "ahr_index_query_keys")
         return keys
+
+
+def _on_stream(stream: Optional[torch.cuda.Stream], device: torch.device, *tensors: torch.Tensor) -> None:
+    """Before a launch on a non-current `stream`: order it after the current stream (which made
+    the inputs and allocated the outputs) and tell the caching allocator that `stream` uses
+    these blocks, so none is recycled before the kernel has consumed or written it."""
+    if stream is None:
+        return
+    cur = torch.cuda.current_stream(device)
+    if stream == cur:
+        return
+    stream.wait_stream(cur)
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(stream)
 
 
 def merge_topk_keys(keys: torch.Tensor, k: int, stream: Optional[torch.cuda.Stream] = None
@@ -288,6 +305,7 @@ def merge_topk_keys(keys: torch.Tensor, k: int, stream: Optional[torch.cuda.Stre
     scores = torch.empty((B, k), dtype=torch.float32, device=dev)
     rows = torch.empty((B, k), dtype=torch.int32, device=dev)
     kout = torch.empty((B, k), dtype=torch.int64, device=dev)
+    _on_stream(stream, dev, keys, scores, rows, kout)
     with torch.cuda.device(dev):
         nat.check(nat.lib().ahr_topk_merge(nat.ptr(keys), B, n_lists, k_in, int(k), nat.ptr(scores),
                                            nat.ptr(rows), nat.ptr(kout), nat.stream_ptr(stream)),

@@ -497,10 +497,12 @@ class HierarchicalGraph:
 
     def _assemble(self, engine: SearchEngine, rows, scores, res, b: int, top_k: int, return_cluster: bool):
         seeds = []
-        for r, s in zip(rows.tolist(), scores.tolist()):
+        # Chroma's cosine distance of a hit is a float32 (hnswlib: 1 - <q, x> in single precision);
+        # the reference turns it into semantic = 1.0 - float(dist) in double (:719-724)
+        dists = (np.float32(1.0) - np.asarray(scores, np.float32)).tolist()
+        for r, dist in zip(rows.tolist(), dists):
             if r < 0:
                 continue
-            dist = 1.0 - float(s)  # Chroma's cosine distance of the hit
             seeds.append({"node_id": engine.row_ids[r], "semantic": 1.0 - float(dist), "meta": engine.row_metas[r]})
         n_nodes = engine.graph.n_nodes
         nodes = self.G.nodes

@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .embeddings import _on_stream
 
 EDGE_TYPES = ("belongs_to", "related_to", "participates_in")
 # CSR list order of include/ahr.h: belongs_to out/in, related_to out/in, participates_in out/in
@@ -167,6 +168,7 @@ class DeviceGraph:
         c = params.to_c()
         sn = seed_nodes.to(device=dev, dtype=torch.int32).contiguous()
         ss = seed_sem.to(device=dev, dtype=torch.float32).contiguous()
+        _on_stream(stream, dev, sn, ss, en, es, ex, ec, on, osem, osc, oc)
         with torch.cuda.device(dev):
             nat.check(nat.lib().ahr_graph_expand_rerank(
                 self._h, nat.ptr(sn), nat.ptr(ss), B, k, nat.ctypes.byref(c), max_exp,
@@ -182,6 +184,7 @@ class DeviceGraph:
         out = torch.empty((B, max(limit, 1)), dtype=torch.int32, device=dev)
         cnt = torch.empty((B,), dtype=torch.int32, device=dev)
         x = inputs.to(device=dev, dtype=torch.int32).contiguous()
+        _on_stream(stream, dev, x, out, cnt)
         with torch.cuda.device(dev):
             nat.check(nat.lib().ahr_graph_expand(self._h, ACTIONS[action], nat.ptr(x), B, n_in, int(limit),
                                                  nat.ptr(out), nat.ptr(cnt), nat.stream_ptr(stream)),
@@ -283,8 +286,12 @@ class SearchEngine:
         k = max(1, params.top_k)
         k_dense = min(k, nat.AHR_MAX_K_LARGE)
         scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
+        if stream is not None:  # the gather below and the host copies run on the current stream
+            torch.cuda.current_stream(self.graph.device).wait_stream(stream)
         valid = rows >= 0
         nodes = torch.where(valid, self.row_to_node[rows.clamp_min(0).long()], torch.full_like(rows, -1))
         res = self.graph.expand_rerank(nodes, scores, params, stream=stream)
+        if stream is not None:
+            torch.cuda.current_stream(self.graph.device).wait_stream(stream)
         host = res.to_host()
         return rows.cpu().numpy(), scores.cpu().numpy(), host

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <string>
 
 namespace ahr {
@@ -17,6 +18,18 @@ int hip_fail(hipError_t e, const char* what);
     hipError_t e_ = (call);                             \
     if (e_ != hipSuccess) return ::ahr::hip_fail(e_, #call); \
   } while (0)
+
+// Opt a kernel into more than 64 KiB of dynamic LDS on the CURRENT device. The attribute is per
+// (function, device), so `done` keeps one bit per device; the atomic makes concurrent first
+// launches from several host threads safe (a duplicate set is harmless).
+inline void ensure_lds_attr(std::atomic<uint64_t>& done, const void* fn, int bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const uint64_t bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
 
 // ---- packed sort keys --------------------------------------------------------------------
 // key = ord(score) << 32 | (0xFFFFFFFF - row): a larger key is a better hit, i.e. the order

@@ -2549,7 +2549,7 @@ __global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __rest
     ptr[u] = 0;
     head[u] = (l < n_lists && k_in > 0) ? kb[l * k_in] : 0;
   }
-  uint64_t mine = 0;  // lane j keeps the j-th winner (k <= 64 here)
+  uint64_t mine = 0;  // lane j % 64 keeps the j-th winner; flushed in windows of 64 outputs
   for (int j = 0; j < k; ++j) {
     uint64_t m = head[0];
 #pragma unroll
@@ -2835,12 +2835,8 @@ template <int DT, int KCAP, int MODE>
 void launch_tile(const ahr_index* ix, int n_splits, int qblocks, int tiles_per_split,
                  int n_row_tiles, int n_rows, int B, int k, uint32_t row_base, const float* thr,
                  float* score_out, int64_t score_ld, int flags, hipStream_t s) {
-  static bool attr_set = false;  // > 64 KiB dynamic LDS needs the opt-in once per kernel
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tile_kernel<DT, KCAP, MODE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(&topk_tile_kernel<DT, KCAP, MODE>), kLdsBytes);
   dim3 grid((unsigned)(n_splits * qblocks));
   hipLaunchKernelGGL((topk_tile_kernel<DT, KCAP, MODE>), grid, dim3(kThreads), kLdsBytes, s,
                      ix->rows, ix->qbuf, ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes,
@@ -2853,12 +2849,8 @@ void launch_lane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
                  const float* thr, int flags, hipStream_t s) {
   using C = lanek::Cfg<NB, BJ, WR, WQ, STAGES>;
   constexpr auto kern = &topk_lane_kernel<DT, KCAP, NB, BJ, WR, WQ, STAGES, MINB>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              C::kLdsTotal);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), C::kLdsTotal);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(C::kThreads), C::kLdsTotal, s, ix->rows,
                      ix->qbuf, ix->row_stride, n_rows, B, ix->d_pad * ix->elem / lanek::kRowBytes, p.n_splits,
                      p.n_row_tiles, row_base, k, ix->part, thr, p.qblocks, flags);
@@ -2872,11 +2864,8 @@ void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B
   static_assert(kTileQ * 4 * KCAP * 8 <= lds, "end merge exchange must fit");
   static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
   constexpr auto kern = &topk_tilelane_kernel<DT, KCAP>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(kThreads), lds, s, ix->rows, ix->qbuf,
                      ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes, p.n_row_tiles, row_base, k,
                      ix->part, thr, p.n_splits, p.qblocks, flags);
@@ -2906,11 +2895,8 @@ void launch_qkv(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int
                 const float* thr, int flags, hipStream_t s) {
   constexpr int lds = qkv::Cfg<ST>::kLds;
   constexpr auto kern = &topk_qkv_kernel<DT, NKT, ST, KCAP>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), lds, s, ix->rows, ix->qbuf,
                      ix->row_stride, n_rows, B, p.n_row_tiles, row_base, k, ix->part, thr, p.n_splits, p.qblocks,
                      flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
@@ -2920,12 +2906,8 @@ template <int DT, int KCAP>
 void launch_t256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                  const float* thr, int flags, hipStream_t s) {
   constexpr auto kern = &topk_t256_kernel<DT, KCAP>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              t256::kLds);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), t256::kLds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), t256::kLds, s, ix->rows, ix->qbuf,
                      ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes, p.n_row_tiles, row_base, k, ix->part,
                      thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
@@ -2959,12 +2941,8 @@ void launch_small(const ahr_index* ix, const SearchPlan& p, const float* q, int 
                   uint32_t row_base, hipStream_t s) {
   constexpr auto kern = &topk_small_kernel<DT, KCAP, NG>;
   const int lds = small::lds_bytes(ix->row_stride, KCAP, NG);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::waves(NG) * 64), lds, s, ix->rows, q, ix->dim,
                      normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, (int)ix->count, B,
                      (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part);
@@ -3094,13 +3072,9 @@ void launch_merge(const uint64_t* in, int B, int n_lists, int k_in, int k, float
     return;
   }
   if (n_lists <= 512 && n_lists * k_in <= kMergeBlockKeys) {
-    static bool attr_set = false;  // up to 64 KiB + 64 B of dynamic LDS
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_block_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kMergeBlockKeys * 8 + 64);
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(merge_block_kernel, dim3(B), dim3(256), (size_t)n_lists * k_in * 8 + 64, s, in, n_lists, k_in,
+    static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+    ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(&merge_block_kernel), kMergeBlockKeys * 8);
+    hipLaunchKernelGGL(merge_block_kernel, dim3(B), dim3(256), (size_t)n_lists * k_in * 8, s, in, n_lists, k_in,
                        k, scores, rows, keys_out);
     return;
   }
@@ -3134,12 +3108,8 @@ int run_query_large_k(ahr_index* ix, int B, int k, uint32_t row_base, float* sco
   int st = ensure_cand(ix, chunk * ld * (int64_t)sizeof(float));
   if (st) return st;
   float* sc = reinterpret_cast<float*>(ix->cand);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_tile_kernel<DT, 8, MODE_SCORES>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(&topk_tile_kernel<DT, 8, MODE_SCORES>), kLdsBytes);
   const int n_row_tiles = (int)cdiv(n, kTileRows);
   prof_mark(ix, 1, s);
   prof_mark(ix, 2, s);

@@ -20,6 +20,13 @@
 #include <cstring>
 #include <vector>
 
+// The rerank reproduces CPython's float64 arithmetic bit for bit: every multiply and add rounds on
+// its own, as in `alpha*sem + beta*jt + ...` evaluated by the interpreter. hipcc contracts a*b + c
+// into one fma by default for device code, which rounds once and can move round(x, 4) across a
+// half-way point; switch contraction off for this whole translation unit (explicit fma() calls,
+// like py_round4's TwoProduct, are unaffected).
+#pragma clang fp contract(off)
+
 namespace ahr {
 namespace graph {
 
@@ -84,7 +91,9 @@ __global__ __launch_bounds__(64) void expand_rerank_kernel(
   for (int s = 0; s < k_seed; ++s) {
     const int32_t nid = seed_nodes[(int64_t)q * k_seed + s];
     if (nid < 0) continue;  // no hit (Chroma returned fewer ids)
-    const double sem = (double)seed_sem[(int64_t)q * k_seed + s];
+    // semantic = 1.0 - float(dist) (:719-724), dist = Chroma's float32 cosine distance 1 - score
+    const float dist = 1.0f - seed_sem[(int64_t)q * k_seed + s];
+    const double sem = 1.0 - (double)dist;
     int pos = -1;
     for (int i = 0; i < n; ++i)
       if (en[i] == nid) { pos = i; break; }

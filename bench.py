@@ -184,7 +184,8 @@ def main() -> None:
         i = counter[0] % depth
         counter[0] += 1
         local.set_workspace(i)
-        return local.query(q, k, stream=streams[i], out=outs[i])
+        with torch.cuda.stream(streams[i]):  # current stream = the batch's stream: no cross-stream wait
+            return local.query(q, k, out=outs[i])
 
     def timed(depth: int) -> float:
         for _ in range(args.warmup):

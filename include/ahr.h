@@ -190,7 +190,8 @@ typedef struct ahr_rerank_params {
 
 /* Batched search() tail: seeds -> 1-hop expansion -> rerank (hierarchical_graph.py:726-782).
  * seed_nodes: device int32 [B][k_seed] (-1 = absent; >= n_nodes = id unknown to the graph);
- * seed_sem: device fp32 [B][k_seed] (semantic = 1 - cosine distance).
+ * seed_sem: device fp32 [B][k_seed], the dense scores; the kernel forms the reference's
+ *   semantic = 1.0 - double(dist) from Chroma's float32 cosine distance dist = 1.0f - score.
  * Outputs (device, per query q):
  *   exp_nodes/exp_sem/exp_src [B][max_exp], exp_count [B]: the `expanded` dict in insertion
  *     order; exp_src = seed index (entry owned by a seed) or -1 - assumed_node_type (added by

@@ -14,7 +14,7 @@ def build(force: bool = False) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
         return LIB
-    cmd = ["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fopenmp", "-shared", "-fPIC",
+    cmd = ["gcc", "-O3", "-mavx2", "-mfma", "-ffp-contract=off", "-fopenmp", "-shared", "-fPIC",
            SRC, "-o", LIB, "-lm"]
     subprocess.run(cmd, check=True)
     return LIB

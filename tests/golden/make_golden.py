@@ -17,7 +17,7 @@ Stand-ins (test scaffolding, not product code):
   * encoder: sha1(text) seeds numpy.default_rng -> standard normal vector, L2-normalised in fp32
     (identical to ah_rag.embeddings.HashEncoder, which the tests check by digest);
   * collection: exhaustive cosine over the stored vectors. Scores are the fp32 fma chain of the
-    C oracle (oracle/ahr_oracle.c, mode 0), distance = 1 - score (Python float), ranking
+    C oracle (oracle/ahr_oracle.c, mode 0), distance = float32(1 - score) as hnswlib returns it, ranking
     (score desc, insertion order asc) — what Chroma returns when its HNSW walk is exhaustive.
 
 Run: python tests/golden/make_golden.py   (needs /root/reference; never runs on the GPU box)
@@ -82,7 +82,8 @@ class StubCollection:
             s = dense_ref.scores_matrix(C, np.asarray([q], np.float32), mode="fma")[0]
             order = sorted(range(len(s)), key=lambda i: (-float(s[i]), i))[:n_results]
             out["ids"].append([self.ids[i] for i in order])
-            out["distances"].append([1.0 - float(s[i]) for i in order])
+            # hnswlib (Chroma's index) returns 1 - <q, x> as a float32 distance
+            out["distances"].append([float(np.float32(1.0) - np.float32(s[i])) for i in order])
             out["metadatas"].append([self.metas[i] for i in order])
             out["documents"].append([self.docs[i] for i in order])
         return out

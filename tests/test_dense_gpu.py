@@ -2,7 +2,8 @@
 
 fp32 mode: bit-exact — rows AND fp32 scores equal the oracle's k-ordered fma chain.
 bf16 / f16: scores within 1e-4 of the double-precision oracle on the same rounded inputs;
-            rows equal except near-ties (exact score gap below 2e-5 at the k-th position).
+            rows equal except near-ties (a differing row's exact score is within 2e-5 of the
+            oracle's score at that rank).
 """
 import numpy as np
 import pytest
@@ -69,9 +70,9 @@ def test_half_precision_vs_f64(cuda, dtype, n, d, B, k):
     assert np.abs(s - es).max() < 1e-4
     mism = r != er
     if mism.any():
-        # every mismatch must be a near-tie at the k-th boundary
-        kth = es[:, -1:]
-        assert (np.abs(got_exact[mism] - np.broadcast_to(kth, r.shape)[mism]) < 2e-5).all()
+        # every mismatch must be a near-tie: the exact score of the row returned at a rank is
+        # within 2e-5 of the oracle's score at that rank (adjacent swap or k-th boundary)
+        assert (np.abs(got_exact[mism] - es[mism]) < 2e-5).all()
 
 
 def test_self_match_rank0(cuda):

@@ -41,7 +41,7 @@ def _oracle_search(G, meta, index, query, params, return_cluster):
     scores, rows = dense_ref.topk(vecs, q, min(k, len(ids)), mode="fma")
     seeds = []
     for s, r in zip(scores[0], rows[0]):
-        dist = 1.0 - float(np.float32(s))
+        dist = float(np.float32(1.0) - np.float32(s))  # Chroma: fp32 distance
         m = dict(metas[r])
         m["updated_at"] = "<ts>"
         seeds.append({"node_id": ids[r], "semantic": 1.0 - float(dist), "meta": m})
