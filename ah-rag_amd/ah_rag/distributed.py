@@ -15,7 +15,8 @@ The reference has no distributed code at all (no NCCL/MPI/Gloo); thi
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import os
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -52,18 +53,53 @@ def all_gather_keys(keys: torch.Tensor, group: Optional[dist.ProcessGroup] = Non
     return out
 
 
+def free_port() -> int:
+    """An unused TCP port on 127.0.0.1 for the rendezvous of spawned ranks."""
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def _rank_entry(local_rank: int, world: int, port: int, target: Callable, args: tuple) -> None:
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+    target(*args)
+
+
+def launch(world: int, target: Callable, args: tuple = ()) -> None:
+    """One process per rank on this node, torch.distributed.run-style environment (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), then target(*args) in each.
+
+    Fresh interpreters (spawn start method): call this BEFORE anything in the parent touches the
+    GPU (a process that initialised HIP must not fork or exec). Raises if any rank fails."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rank_entry, args=(world, free_port(), target, args), nprocs=world, join=True)
+
+
 class ShardedDenseIndex:
-    """This rank's shard of a row-partitioned corpus + the gather/merge query path."""
+    """This rank's shard of a row-partitioned corpus + the gather/merge query path.
+
+    `local` (default: a DenseIndex on this rank's GPU) answers the shard's top-k as packed keys
+    with global row ids; `merge` (default: the on-device ahr_topk_merge) folds the gathered
+    [B, G, k] lists. Both are injectable so the distribution logic runs on CPU ranks with a host
+    stand-in (tests/test_distributed_cpu.py); the product path always uses the defaults."""
 
     def __init__(self, dim: int, n_rows: int, dtype: str = "bf16", group: Optional[dist.ProcessGroup] = None,
-                 device: Optional[torch.device] = None) -> None:
+                 device: Optional[torch.device] = None, local=None, merge: Optional[Callable] = None) -> None:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.n_rows = int(n_rows)
         self.lo, self.hi = shard_bounds(self.n_rows, self.world)[self.rank]
-        self.local = DenseIndex(dim, max(1, self.hi - self.lo), dtype=dtype, device=device)
+        self.local = local if local is not None else DenseIndex(dim, max(1, self.hi - self.lo), dtype=dtype,
+                                                                device=device)
         self.device = self.local.device
+        self._merge = merge or merge_topk_keys
 
     def upsert_global(self, start: int, vectors: torch.Tensor, normalize: bool = False) -> None:
         """Offer global rows [start, start + n); this rank keeps the part inside its shard."""
@@ -78,11 +114,12 @@ class ShardedDenseIndex:
     def query_keys(self, queries: torch.Tensor, k: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         return self.local.query_keys(queries, k, row_base=self.lo, out=out)
 
-    def query(self, queries: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    def query(self, queries: torch.Tensor, k: int, out_keys: Optional[torch.Tensor] = None
+              ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Global top-k of the batch (every rank gets the same answer): scores f32, rows int32."""
-        keys = self.query_keys(queries, k)
-        gathered = all_gather_keys(keys, self.group)          # [G, B, k]
-        s, r, _ = merge_topk_keys(gathered.permute(1, 0, 2).contiguous(), k)
+        keys = self.query_keys(queries, k, out=out_keys)
+        gathered = all_gather_keys(keys, self.group)          # [G, B, k], RCCL over xGMI
+        s, r, _ = self._merge(gathered.permute(1, 0, 2).contiguous(), k)
         return s, r
 
     def close(self) -> None:

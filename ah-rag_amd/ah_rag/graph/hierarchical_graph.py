@@ -12,8 +12,8 @@ in the other. What changes is the retrieval core behind the same signatures:
                       MI355X (ah_rag.graph_search.SearchEngine -> libahr_hip.so) and only builds
                       the result dicts on the host. search_batch() answers many queries per call.
 
-Not carried over: build_from_artifacts (:241-421, LLM/BERTopic ingest; SURVEY §2 marks it out of
-scope) raises NotImplementedError.
+build_from_artifacts (:241-421) assembles the graph from an artifacts directory; the offline C1
+ingest (ah_rag.ingest) feeds it the deterministic extractor's extractions.json.
 
 Caching: the device index and device graph are built on first search and reused. Mutations made
 through this class's add_* methods invalidate them; after editing self.G directly, call
@@ -223,8 +223,107 @@ class HierarchicalGraph:
         self._touch()
 
     def build_from_artifacts(self, artifacts_dir: str = ARTIFACT_DIR) -> None:
-        raise NotImplementedError("LLM/BERTopic ingest is outside the MI355X retrieval core (SURVEY §2 row 1); "
-                                  "build the graph with the reference pipeline and load() it here")
+        """Assemble the graph from an ingest artifacts directory (reference :241-421).
+
+        Reads whichever of topics.json (entity_to_parents, l1_nodes), l1_nodes.json, l1_edges.json,
+        l1_judge_nodes.json, l1_judge_edges.json, extractions.json, l2_nodes.json and l1_to_l2.json
+        exist, in the reference's order of node and edge insertion (it fixes networkx adjacency
+        order, which search()'s [:2] / [:member_top_m] truncations see). The
+        offline C1 path has extractions.json only (ah_rag.extract): entities, hyperedges and
+        participates_in edges."""
+        def read(name: str, default):
+            path = os.path.join(artifacts_dir, name)
+            if not os.path.exists(path):
+                return default
+            with open(path, encoding="utf-8") as f:
+                return json.load(f)
+
+        topics = read("topics.json", {})
+        entity_to_parents: Dict[str, List[Dict[str, Any]]] = topics.get("entity_to_parents", {}) if topics else {}
+        l1_nodes = read("l1_nodes.json", topics.get("l1_nodes", []) if topics else [])
+        l1_edges = read("l1_edges.json", [])
+        judge_nodes = read("l1_judge_nodes.json", [])
+        judge_edges = read("l1_judge_edges.json", [])
+        extractions = read("extractions.json", [])
+        l2_nodes = read("l2_nodes.json", [])
+        l1_to_l2 = read("l1_to_l2.json", {})
+
+        # entity facts gathered from every extraction: distinct descriptions, first-seen type
+        facts: Dict[str, Dict[str, Any]] = {}
+        for rec in extractions:
+            for ent in rec.get("entities", []):
+                name = ent.get("name")
+                if not name:
+                    continue
+                f = facts.setdefault(name, {"descriptions": [], "entity_type": ent.get("type")})
+                desc = ent.get("description")
+                if desc and desc not in f["descriptions"]:
+                    f["descriptions"].append(desc)
+
+        def joined(name: str) -> Optional[str]:
+            descs = facts.get(name, {}).get("descriptions", [])
+            return "; ".join(descs) if descs else None
+
+        # entities with topic parents first (their order), then the rest in extraction order
+        for name, parents in entity_to_parents.items():
+            self.add_entity(name=name, description=joined(name), entity_type=facts.get(name, {}).get("entity_type"),
+                            embedding_ref=(os.path.join(ARTIFACT_DIR, "embeddings.npy"), -1),
+                            l1_parents={str(p.get("topic_id")): p.get("prob") for p in parents})
+        for name, f in facts.items():
+            if name not in entity_to_parents:
+                self.add_entity(name=name, description=joined(name), entity_type=f.get("entity_type"))
+        for node in l1_nodes:
+            self.add_summary(topic_id=int(node.get("topic_id")), title=node.get("title"),
+                             summary_text=node.get("summary") or node.get("summary_text"),
+                             confidence=node.get("confidence"), top_words=node.get("top_words") or [],
+                             members=node.get("members") or [], centroid=node.get("centroid"))
+        for name, parents in entity_to_parents.items():
+            eid = self.name_to_entity_id.get(name)
+            if not eid:
+                continue
+            for p in parents:
+                sid = self.topic_to_summary_id.get(int(p.get("topic_id")))
+                if sid:
+                    self.add_belongs_to(eid, sid, prob=p.get("prob"))
+        for e in l1_edges:
+            a = self.topic_to_summary_id.get(int(e.get("source")))
+            b = self.topic_to_summary_id.get(int(e.get("target")))
+            if a and b:
+                self.add_related(a, b, weight=e.get("weight"), jaccard=e.get("jaccard"), cosine=e.get("cosine"),
+                                 overlap=e.get("overlap"), confidence=e.get("confidence"))
+        for i, rec in enumerate(extractions):
+            uid = rec.get("id")
+            if uid is None:
+                uid = "hedge_%d_%s" % (i, rec.get("relation_type", "unknown"))
+            hid = self.add_hyperedge(uid=str(uid), description=rec.get("hyperedge"),
+                                     relation_type=rec.get("relation_type"),
+                                     confidence_score=rec.get("confidence_score"))
+            for ent in rec.get("entities", []):
+                eid = self.name_to_entity_id.get(ent.get("name")) if ent.get("name") else None
+                if eid:
+                    self.add_participation(eid, hid, role=ent.get("role") if isinstance(ent, dict) else None)
+        if l2_nodes:
+            for n in l2_nodes:
+                sid = self.add_summary(topic_id=int(n.get("topic_id")), title=n.get("title"),
+                                       summary_text=n.get("summary"), confidence=n.get("confidence"),
+                                       top_words=n.get("top_words"), members=n.get("members"),
+                                       centroid=n.get("centroid"))
+                self.G.nodes[sid]["level"] = 2
+            for l1_key, l2_tid in l1_to_l2.items():
+                try:
+                    l1_sid = self.topic_to_summary_id.get(int(l1_key))
+                except (TypeError, ValueError):
+                    continue
+                l2_sid = self.topic_to_summary_id.get(int(l2_tid))
+                if l1_sid and l2_sid:
+                    self.add_belongs_to(l1_sid, l2_sid, prob=1.0)
+        by_topic = {int(d.get("topic_id")): n for n, d in self.G.nodes(data=True) if d.get("node_type") == "summary"}
+        for js in judge_nodes:
+            nid = by_topic.get(int(js.get("id")))
+            if nid:
+                self.G.nodes[nid]["judge_scores"] = json.dumps(js)
+        if judge_edges:
+            self.G.graph["judge_edges"] = judge_edges
 
     def invalidate_device_cache(self) -> None:
         self._version += 1

@@ -94,3 +94,43 @@ class SyntheticCorpus:
         q = _normalize(base + scale * eps)
         source = torch.cat([src, torch.full((batch - half,), -1, dtype=torch.int64)])
         return q, source
+
+
+def build_hotpot_graph(corpus: SyntheticCorpus, rng: Optional[np.random.Generator] = None,
+                       n_hyper: int = 40_000):
+    """HotpotQA-distractor-shaped HierarchicalGraph over the corpus rows: one summary
+    per topic (the first n_summaries topics), 1-2 belongs_to parents per entity, ~2 related_to per
+    summary, n_hyper unindexed hyperedges of 2-5 same-topic participants. Returns (graph, ids),
+    ids[r] = node id of corpus row r (entities first, then summaries, the rows() order)."""
+    from .graph.hierarchical_graph import HierarchicalGraph
+    rng = rng if rng is not None else np.random.default_rng(SEED)
+    s = corpus.spec
+    topics = corpus.topics.numpy()
+    hg = HierarchicalGraph()
+    sids = [hg.add_summary(t, title=f"Topic {t}", summary_text=f"summary of topic {t}",
+                           confidence=float(rng.uniform(5, 10)), top_words=[f"w{t}", f"v{t}"],
+                           judge_scores={"overall": float(rng.uniform(0, 10))}) for t in range(s.n_summaries)]
+    eids = [hg.add_entity(f"entity {i}", description=f"entity {i} of topic {topics[i]}", entity_type="thing")
+            for i in range(s.n_entities)]
+    second = rng.integers(0, s.n_summaries, s.n_entities)
+    for i, e in enumerate(eids):
+        hg.add_belongs_to(e, sids[topics[i] % s.n_summaries], prob=0.9)
+        if second[i] != topics[i] % s.n_summaries:
+            hg.add_belongs_to(e, sids[second[i]], prob=0.1)
+    for t in range(s.n_summaries):
+        for u in rng.integers(0, s.n_summaries, 2):
+            if u != t:
+                hg.add_related(sids[t], sids[u], weight=0.5)
+    by_topic: dict = {}
+    for i, t in enumerate(topics):
+        by_topic.setdefault(int(t), []).append(i)
+    for h in range(n_hyper):
+        pool = by_topic.get(int(rng.integers(0, s.n_centroids)))
+        if not pool:
+            continue
+        k = min(len(pool), int(rng.integers(2, 6)))  # mean ~3.5-3.8 participants
+        hid = hg.add_hyperedge(f"h{h}", description=f"relation {h}", relation_type="rel",
+                               confidence_score=float(rng.uniform(0, 1)))
+        for i in rng.choice(pool, k, replace=False):
+            hg.add_participation(eids[int(i)], hid)
+    return hg, eids + sids

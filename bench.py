@@ -2,18 +2,26 @@
 """bench.py — headline benchmark of the MI355X dense-retrieval hot path.
 
 Metric (BASELINE.json): queries/sec + recall@10, d=768 HotpotQA corpus, 1/2/4/8 MI355X.
-Workload (default, BASELINE.json configs[1]): HotpotQA-distractor-shaped graph corpus,
-90,000 rows (87k entity + 3k summary) x d=768 stored bf16 in HBM, batch of 1,024 queries,
-exact top-10 by inner product of L2-normalised vectors (= cosine), fused Q.N^T + top-k kernel.
-One step = one batch through ahr_index_query (query conversion, threshold pre-pass, fused tile
-kernel, cross-split merge). Inputs are resident in HBM before the timed region.
 
---workload synth5m runs configs[2] (5M x 768 fp16). --gpus N (launched by torch.distributed.run)
-runs one process per GPU: --shard queries (default) gives every rank a corpus replica and its own
-query batch (weak scaling, no collective on the data path); --shard rows splits the corpus rows
-across ranks and merges the per-rank top-k with an RCCL all-gather (strong scaling, configs[3]).
+N = 1 (default; BASELINE.json configs[1]): HotpotQA-distractor-shaped corpus, 90,000 rows (87k
+entity + 3k summary) x d=768 stored bf16 in HBM, batches of 1,024 queries, exact top-10 by inner
+product of L2-normalised vectors (= cosine). One step = one batch through ahr_index_query (query
+conversion, threshold pre-pass, fused MFMA Q.N^T + top-k tile kernel, cross-split merge). Inputs
+are resident in HBM before the timed region.
 
-The data is synthetic (no dataset or encoder weights offline).
+N > 1 (BASELINE.json configs[3]): the 5M x 768 fp16 corpus (configs[2]) row-sharded over the N
+GPUs of the node, one process per GPU. One step = local fused top-k on every rank -> RCCL
+all-gather of the [B, 10] packed keys over xGMI -> on-device merge, all inside the timed region
+(strong scaling: the job answers B queries per step). rank 0 also times the unsharded 5M search
+on its own GPU in the same run (config.n1_same_workload_qps). `--shard queries` is the replica
+mode instead (every rank a full corpus and its own batches, weak scaling).
+
+Launch: the driver's `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`, or
+plain `python bench.py --gpus N`, which spawns the N rank processes itself before any GPU call.
+
+The data is synthetic (no dataset or encoder weights offline). recall@10 is
+measured against the exact fp32 ground truth of the fp32 source vectors, computed on the host
+with numpy/BLAS (the reference's numpy path), on a sample of the batch.
 """
 from __future__ import annotations
 
@@ -33,35 +41,68 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from ah_rag.distributed import ShardedDenseIndex, all_gather_keys  # noqa: E402
-from ah_rag.embeddings import DenseIndex, merge_topk_keys  # noqa: E402
+from ah_rag.distributed import ShardedDenseIndex, launch  # noqa: E402
+from ah_rag.embeddings import DenseIndex  # noqa: E402
 from ah_rag.synthetic import HOTPOT_90K, SYNTH_5M, SyntheticCorpus  # noqa: E402
 
 METRIC = "queries/sec + recall@10, d=768 HotpotQA corpus, 1/2/4/8 MI355X"
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f16": 2500.0, "f32": 157.3}  # MI355X_MICROARCH.md, dense
 HBM_PEAK_GBS = 8000.0
+KERNEL_NAMES = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
+                "tilelane128": "topk_tilelane_kernel", "t256": "topk_t256_kernel",
+                "qkv128": "topk_qkv_kernel"}
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["hotpot90k", "synth5m"], default="hotpot90k")
+    ap.add_argument("--workload", choices=["hotpot90k", "synth5m"], default=None,
+                    help="default: hotpot90k at N=1, synth5m (row-sharded) at N>1")
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--dtype", choices=["bf16", "f16", "f32"], default=None)
-    ap.add_argument("--shard", choices=["queries", "rows"], default="queries")
+    ap.add_argument("--shard", choices=["queries", "rows"], default=None,
+                    help="N>1: rows (default; configs[3]) or queries (replicas)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (default); gloo only to rehearse several ranks on one GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (s)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per leg (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-n1-ref", action="store_true", help="rows mode: skip the unsharded rank-0 timing")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (one stream + index workspace each); rows-sharded runs use 1")
     ap.add_argument("--recall-queries", type=int, default=256)
     ap.add_argument("--debug-flags", type=int, default=0,
                     help="ablation/kernel-selection switches (DenseIndex.set_debug_flags); 0 in production")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------------------------
+# host-side numpy path (the reference's CPU math: BLAS fp32 + argpartition, tie rule score desc /
+# row asc) — used for the recall ground truth and timed as the CPU baseline
+# ---------------------------------------------------------------------------------------------
+def numpy_topk(corpus: np.ndarray, queries: np.ndarray, k: int, row_base: int = 0):
+    s = np.asarray(queries, np.float32) @ np.asarray(corpus, np.float32).T
+    k_eff = min(k, s.shape[1])
+    part = np.argpartition(-s, k_eff - 1, axis=1)[:, :k_eff]
+    ps = np.take_along_axis(s, part, axis=1)
+    idx = np.empty_like(part)
+    for b in range(s.shape[0]):
+        idx[b] = part[b][np.lexsort((part[b], -ps[b]))]
+    return np.take_along_axis(s, idx, axis=1), idx.astype(np.int64) + row_base
+
+
+def numpy_topk_chunked(rows: torch.Tensor, queries: np.ndarray, k: int, chunk: int = 250_000):
+    """Exact fp32 top-k over a device-resident corpus too large for one host copy."""
+    best_s = np.full((len(queries), k), -np.inf, np.float32)
+    best_r = np.full((len(queries), k), -1, np.int64)
+    for s0 in range(0, rows.shape[0], chunk):
+        cs, cr = numpy_topk(rows[s0:s0 + chunk].cpu().numpy(), queries, k, row_base=s0)
+        alls, allr = np.concatenate([best_s, cs], 1), np.concatenate([best_r, cr], 1)
+        order = np.lexsort((allr, -alls), axis=1)[:, :k]
+        best_s, best_r = np.take_along_axis(alls, order, 1), np.take_along_axis(allr, order, 1)
+    return best_s, best_r
 
 
 def recall_at_k(got: np.ndarray, exact: np.ndarray) -> float:
@@ -70,39 +111,86 @@ def recall_at_k(got: np.ndarray, exact: np.ndarray) -> float:
     return float(np.mean(hits) / k)
 
 
-def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float) -> dict:
-    """The reference math on the host: fp32 BLAS Q @ C.T + argpartition top-k (oracle port)."""
-    from oracle import dense_ref  # checker / baseline only
-
+def host_info() -> dict:
+    info = {"os_cpu_count": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        info["cgroup_cpu_quota"] = None if quota == "max" else round(int(quota) / int(period), 2)
+    except Exception:
+        pass
     try:
         from threadpoolctl import threadpool_info
         blas = [i for i in threadpool_info() if i.get("user_api") == "blas"]
-        threads = int(blas[0]["num_threads"]) if blas else 1
-        blas_name = f"{blas[0].get('internal_api')} {blas[0].get('version')}" if blas else "unknown"
+        if blas:
+            info["blas"] = f"{blas[0].get('internal_api')} {blas[0].get('version')}"
+            info["blas_threads"] = int(blas[0]["num_threads"])
     except Exception:
-        threads, blas_name = int(os.environ.get("OMP_NUM_THREADS", "1")), "unknown"
-    chunk = 256
-    done, t0 = 0, time.perf_counter()
-    i = 0
-    while True:
-        qs = queries[(i * chunk) % len(queries):][:chunk]
-        dense_ref.topk_numpy(rows, qs, k)
-        done += len(qs)
-        i += 1
-        if time.perf_counter() - t0 >= budget_s and done >= chunk:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 2), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": (f"{done} queries in {chunk}-query batches over the full {rows.shape[0]}x{rows.shape[1]} "
-                       f"fp32 corpus, numpy BLAS ({blas_name}, {threads} threads) + argpartition top-{k}; "
-                       f"{dt:.1f}s; host os.cpu_count()={os.cpu_count()}")}
+        pass
+    return info
+
+
+def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float, workload: str) -> dict:
+    """The reference math on the host (BASELINE.md "CPU baseline plan"): fp32 BLAS Q @ C.T +
+    argpartition top-k over the full corpus on all of the process's host threads, at B = 1024 and
+    B = 1, and — for the HotpotQA-shaped graph — the same B = 1024 batches followed by the
+    reference 1-hop expansion + rerank (hierarchical_graph.py:726-782, restated in
+    oracle/search_ref.py) per query."""
+    info = host_info()
+    threads = info.get("blas_threads", int(os.environ.get("OMP_NUM_THREADS", "1")))
+
+    def timed(bsz, extra=None, budget=budget_s):
+        done, i, t0 = 0, 0, time.perf_counter()
+        while True:
+            off = (i * bsz) % max(1, len(queries) - bsz + 1)
+            qs = queries[off:off + bsz]
+            s, r = numpy_topk(rows, qs, k)
+            if extra is not None:
+                extra(s, r)
+            done += len(qs)
+            i += 1
+            if time.perf_counter() - t0 >= budget and done >= bsz:
+                break
+        return done, time.perf_counter() - t0
+
+    n_b, t_b = timed(min(1024, len(queries)))
+    n_1, t_1 = timed(1, budget=budget_s / 2)
+    out = {"value": round(n_b / t_b, 2), "unit": "queries/s", "cores": threads, "kind": "port",
+           "b1_queries_per_s": round(n_1 / t_1, 2)}
+    sample = (f"B=1024: {n_b} queries over the full {rows.shape[0]}x{rows.shape[1]} fp32 corpus, numpy BLAS "
+              f"({info.get('blas', 'unknown')}, {threads} threads) + argpartition top-{k}, {t_b:.1f}s; "
+              f"B=1: {n_1} single-query calls, {t_1:.1f}s")
+    if workload == "hotpot90k":
+        from oracle import search_ref  # CPU baseline leg only
+        from ah_rag.synthetic import build_hotpot_graph
+        corpus = SyntheticCorpus(HOTPOT_90K, torch.device("cpu"))
+        hg, ids = build_hotpot_graph(corpus)
+        p = search_ref.resolve_params({}, top_k=k)
+
+        def rerank(s, r):
+            for sb, rb in zip(s, r):
+                dist_ = (np.float32(1.0) - sb.astype(np.float32)).tolist()
+                seeds = [{"node_id": ids[j], "semantic": 1.0 - float(dd), "meta": {}} for j, dd in zip(rb, dist_)]
+                search_ref.expand_rerank(hg.G, seeds, p, return_cluster=False)
+
+        n_r, t_r = timed(min(1024, len(queries)), rerank)
+        out["with_expand_rerank_queries_per_s"] = round(n_r / t_r, 2)
+        sample += (f"; dense + R5/R7 expansion + rerank (synthetic {hg.G.number_of_nodes()}-node graph): "
+                   f"{n_r} queries, {t_r:.1f}s")
+    out["sample"] = sample + f"; host {json.dumps(info)}"
+    out["host"] = info
+    return out
 
 
 def read_traffic(kernel: str, workload: str, batch: int):
-    """Per-launch HBM bytes of `kernel` from the committed PMC summary (profiles/), if it was
-    measured on this workload and batch (else None)."""
-    paths = [os.path.join(ROOT, "profiles", "pmc_traffic.json")]
-    paths += sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*", "pmc_traffic.json")))
+    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary (profiles/) measured
+    on this workload and batch (else None)."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*", "pmc_traffic.json")), reverse=True)
+    paths.append(os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     for path in paths:
         try:
             with open(path) as f:
@@ -117,14 +205,14 @@ def read_traffic(kernel: str, workload: str, batch: int):
     return None
 
 
-def main() -> None:
-    args = parse_args()
+def run(args) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    workload = args.workload or ("synth5m" if world > 1 else "hotpot90k")
+    shard = args.shard or ("rows" if world > 1 else "queries")
     dev_index = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -135,13 +223,13 @@ def main() -> None:
         else:
             dist.init_process_group("gloo")
 
-    spec = HOTPOT_90K if args.workload == "hotpot90k" else SYNTH_5M
-    dtype = args.dtype or ("bf16" if args.workload == "hotpot90k" else "f16")
+    spec = HOTPOT_90K if workload == "hotpot90k" else SYNTH_5M
+    dtype = args.dtype or ("bf16" if workload == "hotpot90k" else "f16")
     B, k = args.batch, args.k
     corpus = SyntheticCorpus(spec, dev)
     rows = corpus.rows()
     N, d = rows.shape
-    sharded = args.shard == "rows" and world > 1
+    sharded = shard == "rows" and world > 1
     if sharded:
         index = ShardedDenseIndex(d, N, dtype=dtype, device=dev)
         lo, hi = index.lo, index.hi
@@ -155,10 +243,8 @@ def main() -> None:
             local.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
     if args.debug_flags:
         local.set_debug_flags(args.debug_flags)
-    salt = rank if args.shard == "queries" else 0
+    salt = rank if shard == "queries" else 0
     q, src = corpus.queries(B, rows, salt=salt)
-    index.reserve(B, k)
-    keys = torch.empty((B, k), dtype=torch.int64, device=dev)
     # Batches in flight: batch i runs on stream i % inflight with index workspace i % inflight,
     # so the latency-bound stages of one batch (query conversion, pre-pass k-th selection, merge,
     # launch gaps) overlap the neighbouring batch's tile kernel. Every batch still runs the whole
@@ -167,6 +253,7 @@ def main() -> None:
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(inflight - 1)]
     outs = [(torch.empty((B, k), dtype=torch.float32, device=dev), torch.empty((B, k), dtype=torch.int32, device=dev))
             for _ in range(inflight)]
+    keys = torch.empty((B, k), dtype=torch.int64, device=dev)
     for i in range(inflight):
         local.set_workspace(i)
         local.reserve(B, k)
@@ -176,11 +263,8 @@ def main() -> None:
     counter = [0]
 
     def step(depth: int):
-        if sharded:
-            index.query_keys(q, k, out=keys)
-            gathered = all_gather_keys(keys)                  # RCCL all-gather over xGMI
-            s_, r_, _ = merge_topk_keys(gathered.permute(1, 0, 2).contiguous(), k)
-            return s_, r_
+        if sharded:  # local top-k -> RCCL all-gather over xGMI -> device merge
+            return index.query(q, k, out_keys=keys)
         i = counter[0] % depth
         counter[0] += 1
         local.set_workspace(i)
@@ -209,6 +293,7 @@ def main() -> None:
     local.set_workspace(0)
     res = step(1)
     torch.cuda.synchronize()
+    got_rows = res[1].cpu().numpy().astype(np.int64)
     # Stage timings (HIP events between the kernels of a step) in a separate, untimed pass: the
     # event records themselves add ~6 us of GPU-side gap per stage boundary.
     local.profile_begin(args.steps)
@@ -225,25 +310,36 @@ def main() -> None:
     q_per_step = B * world if not sharded else B
     value = q_per_step * args.steps / dt
 
-    # ---- recall@10 against exact fp32 ground truth of the fp32 source vectors (untimed)
-    got_rows = res[1].cpu().numpy().astype(np.int64)
-    nq = min(args.recall_queries, B)
-    if N <= 200_000:
-        from oracle import dense_ref
-        _, exact = dense_ref.topk_numpy(rows.cpu().numpy(), q[:nq].cpu().numpy(), k)
-    else:
-        gt = DenseIndex(d, N, dtype="f32", device=dev)
-        for s in range(0, N, 1_000_000):
-            gt.upsert(rows[s:s + 1_000_000], start=s)
-        exact = gt.query(q[:nq], k)[1].cpu().numpy().astype(np.int64)
-        gt.close()
-    if sharded:
-        got_global = got_rows[:nq]
-    else:
-        got_global = got_rows[:nq] + lo
-    rec = recall_at_k(got_global, exact)
+    # the same workload unsharded on rank 0's GPU, same run (the N = 1 point of the C4 curve)
+    n1_qps = None
+    if sharded and rank == 0 and not args.no_n1_ref:
+        full = DenseIndex(d, N, dtype=dtype, device=dev)
+        for s0 in range(0, N, 1_000_000):
+            full.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
+        full.reserve(B, k)
+        for _ in range(max(2, args.warmup)):
+            full.query(q, k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            full.query(q, k)
+        torch.cuda.synchronize()
+        n1_qps = B * args.steps / (time.perf_counter() - t0)
+        full.close()
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
+        # ---- recall@10 against exact fp32 ground truth of the fp32 source vectors (untimed)
+        nq = min(args.recall_queries if N <= 200_000 else min(args.recall_queries, 128), B)
+        qh = q[:nq].cpu().numpy()
+        if N <= 200_000:
+            _, exact = numpy_topk(rows.cpu().numpy(), qh, k)
+        else:
+            _, exact = numpy_topk_chunked(rows, qh, k)
+        got_global = got_rows[:nq] if sharded else got_rows[:nq] + lo
+        rec = recall_at_k(got_global, exact)
+
         calls = max(1, prof["calls"])
         tile_ms = prof["ms_sum"]["tile_topk"] / calls
         n_local = hi - lo
@@ -253,10 +349,9 @@ def main() -> None:
         elem = 4 if dtype == "f32" else 2
         alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
         plan = local.plan(B, k)
-        kname = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
-                 "tilelane128": "topk_tilelane_kernel", "t256": "topk_t256_kernel",
-                 "small": "topk_small_f32_kernel" if dtype == "f32" else "topk_small_kernel",
-                 "qkv128": "topk_qkv_kernel"}.get(plan["kernel"], "topk_tile_kernel")
+        kname = KERNEL_NAMES.get(plan["kernel"], "topk_tile_kernel")
+        if plan["kernel"] == "small":
+            kname = "topk_small_f32_kernel" if dtype == "f32" else "topk_small_kernel"
         # arithmetic intensity 2*B*N*d / (N*d*elem) against the ridge (peak flops / HBM bytes):
         # small batches are bound by the corpus stream
         hbm_bound = flops / alg_bytes < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
@@ -270,44 +365,59 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if not sharded else "strong",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic (SURVEY.md §8d clustered generator, seed 20251003; no HotpotQA/encoder offline)",
             "recall_at_10": round(rec, 4),
             "config": {
                 "workload": ("hotpot90k: HotpotQA-distractor-shaped corpus 87k entity + 3k summary rows"
-                             if args.workload == "hotpot90k" else "synth5m: 5M-row synthetic corpus"),
+                             if workload == "hotpot90k" else "synth5m: 5M-row synthetic corpus"),
                 "corpus_rows": N, "dim": d, "batch": B, "top_k": k, "index_dtype": dtype,
                 "parallelism": (f"rows{world}" if sharded else (f"queries{world}" if world > 1 else "single")),
                 "launch": plan,
                 "inflight": inflight,
                 "serial_ms_per_step": round(dt_serial / args.steps * 1e3, 4) if dt_serial else None,
+                "recall_queries": nq,
             },
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
             "roofline": {
-                "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} Q.N^T + top-k, {plan['kernel']})",
+                "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} "
+                          f"Q.N^T + top-k, {plan['kernel']})",
                 "bound": "hbm" if hbm_bound else "mfma",
                 "achieved": round(hbm_gbs if hbm_bound else achieved_tf, 2),
                 "peak": HBM_PEAK_GBS if hbm_bound else peak,
                 "unit": "GB/s" if hbm_bound else "TFLOP/s",
                 "frac": round(hbm_gbs / HBM_PEAK_GBS if hbm_bound else achieved_tf / peak, 4),
-                "traffic": read_traffic(kname, args.workload, B),
+                "traffic": read_traffic(kname, workload, B),
                 "algorithmic_flops_per_launch": flops,
                 "algorithmic_bytes_per_launch": alg_bytes,
-                "hbm_equiv_GBs": round(alg_bytes / (tile_ms * 1e-3) / 1e9, 1),
+                "hbm_equiv_GBs": round(hbm_gbs, 1),
                 "avg_launch_ms": round(tile_ms, 5),
             },
             "cpu_baseline": None,
         }
+        if sharded:
+            out["config"]["n1_same_workload_qps"] = round(n1_qps, 1) if n1_qps else None
+            out["config"]["shard_rows"] = n_local
         if world == 1 and not args.no_cpu_baseline:
             nc = min(len(q), 1024)
-            out["cpu_baseline"] = cpu_baseline(rows.cpu().numpy(), q[:nc].cpu().numpy(), k, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(rows.cpu().numpy(), q[:nc].cpu().numpy(), k, args.cpu_seconds,
+                                               workload)
         print(json.dumps(out), flush=True)
     index.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main() -> None:
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, spawned before this process touches the GPU
+        launch(args.gpus, run, (args,))
+        return
+    run(args)
 
 
 if __name__ == "__main__":

@@ -27,38 +27,7 @@ import torch  # noqa: E402
 from ah_rag.agent.gym_env import AHRAGGymEnv  # noqa: E402
 from ah_rag.agent.vec_env import VecAHRAGGymEnv  # noqa: E402
 from ah_rag.graph.hierarchical_graph import HierarchicalGraph, VectorStore  # noqa: E402
-from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus  # noqa: E402
-
-
-def build_graph(corpus: SyntheticCorpus, rng: np.random.Generator, n_hyper: int = 40_000):
-    s = corpus.spec
-    topics = corpus.topics.numpy()
-    hg = HierarchicalGraph()
-    sids = [hg.add_summary(t, title=f"Topic {t}", summary_text=f"summary of topic {t}",
-                           confidence=float(rng.uniform(5, 10)), top_words=[f"w{t}", f"v{t}"],
-                           judge_scores={"overall": float(rng.uniform(0, 10))}) for t in range(s.n_summaries)]
-    eids = [hg.add_entity(f"entity {i}", description=f"entity {i} of topic {topics[i]}", entity_type="thing")
-            for i in range(s.n_entities)]
-    second = rng.integers(0, s.n_summaries, s.n_entities)
-    for i, e in enumerate(eids):
-        hg.add_belongs_to(e, sids[topics[i] % s.n_summaries], prob=0.9)
-        if second[i] != topics[i] % s.n_summaries:
-            hg.add_belongs_to(e, sids[second[i]], prob=0.1)
-    for t in range(s.n_summaries):
-        for u in rng.integers(0, s.n_summaries, 2):
-            if u != t:
-                hg.add_related(sids[t], sids[u], weight=0.5)
-    by_topic = {}
-    for i, t in enumerate(topics):
-        by_topic.setdefault(int(t), []).append(i)
-    for h in range(n_hyper):
-        pool = by_topic[int(rng.integers(0, s.n_centroids))]
-        k = min(len(pool), int(rng.integers(2, 6)))  # mean ~3.5-3.8 participants
-        hid = hg.add_hyperedge(f"h{h}", description=f"relation {h}", relation_type="rel",
-                               confidence_score=float(rng.uniform(0, 1)))
-        for i in rng.choice(pool, k, replace=False):
-            hg.add_participation(eids[int(i)], hid)
-    return hg, eids + sids
+from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph  # noqa: E402
 
 
 def install_vectors(hg: HierarchicalGraph, ids, vectors: np.ndarray, db_path: str) -> None:
@@ -88,7 +57,7 @@ def main():
     t0 = time.perf_counter()
     corpus = SyntheticCorpus(HOTPOT_90K, dev)
     vectors = corpus.rows().cpu().numpy()
-    hg, ids = build_graph(corpus, rng)
+    hg, ids = build_hotpot_graph(corpus, rng)
     tmp = tempfile.mkdtemp(prefix="ahr_env_")
     install_vectors(hg, ids, vectors, os.path.join(tmp, "vector_db"))
     q, _ = corpus.queries(a.envs, corpus.rows())
