@@ -190,8 +190,11 @@ enum {
   kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
   kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
   kFlagSmallWide = 65536,  // the small-batch kernel up to B = 64 (2 or 4 query groups; measured slower)
+  kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
+  kFlagNoKB256 = 262144,  // plan without the k-blocked kernel
 };
-constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256;
+constexpr int kKernelFlags =
+    kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 | kFlagKB256 | kFlagNoKB256;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
@@ -1317,6 +1320,281 @@ __global__ __launch_bounds__(512, 1) void topk_t256_kernel(
       // passing groups, one static group at a time (skipped unless some lane passes it): the
       // pass mask and the passing values come straight from the accumulators (select chain), no
       // LDS round trip
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const int nb = g >> 1, mh = g & 1;
+        if (!__ballot((gmask >> g) & 1u)) continue;
+        if ((gmask >> g) & 1u) {
+          const int rb = r0 + mh * 64 + fq * 4;  // value 4u + i: row rb + 16u + i
+          uint32_t pm = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              pm |= (acc[4 * mh + u][nb][i] >= thr[nb] && rb + 16 * u + i < n_rows ? 1u : 0u) << (4 * u + i);
+          while (pm) {
+            const int r = __builtin_ctz(pm);
+            pm &= pm - 1;
+            float v = acc[4 * mh][nb][0];
+#pragma unroll
+            for (int rr = 1; rr < 16; ++rr) v = (r == rr) ? acc[4 * mh + (rr >> 2)][nb][rr & 3] : v;
+            const uint64_t key = make_key(v, row_base + (uint32_t)(rb + 16 * (r >> 2) + (r & 3)));
+            if (key > thk[nb]) {
+              if (stash[nb] == 0) {
+                stash[nb] = key;
+              } else if (nc[nb] < cand_cap) {
+                cand_keys[cbase(nb) + nc[nb]] = key;
+                ++nc[nb];
+              } else {
+                list_push(nb, key);
+              }
+            }
+          }
+        }
+      }
+    }
+    if (flags & kFlagSkipEpilogue) {
+      float sink = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) sink += acc[mb][nb][0] + acc[mb][nb][3];
+      if (sink == 1234.5678f) part_keys[0] = 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
+  }
+
+  // per query slot: fold the candidate keys into a register list, merge the 4 lane quarters
+  // (lanes fr, fr + 16, fr + 32, fr + 48: disjoint rows of one query), write one list per
+  // (query, split, row half)
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int q = q0 + wn * 64 + nb * 16 + fr;
+    uint64_t L[KCAP];
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[j] = Ls[nb][j];
+    if (stash[nb]) list_insert<KCAP>(L, stash[nb]);
+    const int n = nc[nb];
+    const int64_t cb = q < n_q ? cbase(nb) : 0;
+    for (int g0 = 0; g0 < n; g0 += 8) {
+      uint64_t c8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c8[u] = g0 + u < n ? cand_keys[cb + g0 + u] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c8[u]) list_insert<KCAP>(L, c8[u]);
+    }
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      uint64_t P[KCAP];
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) P[j] = shfl_xor_u64(L[j], m);
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j) list_insert<KCAP>(L, P[j]);
+    }
+    if (fq == 0 && q < n_q) {
+      uint64_t* dst = part_keys + ((int64_t)q * (2 * n_splits) + 2 * split + wm) * k_out;
+#pragma unroll
+      for (int j = 0; j < KCAP; ++j)
+        if (j < k_out) dst[j] = L[j];
+    }
+  }
+}
+
+// =============================================================================================
+// topk_kb256_kernel (bf16/f16, k <= 16; the default from B = 17): the t256 tile (256 corpus rows x
+// 256 queries, 8 waves = 2 along rows x 4 along queries, a 128 x 64 block of 16x16x32 MFMAs per
+// wave, 128 accumulator VGPRs, one workgroup per CU) fed from a K-BLOCKED copy of the corpus and
+// of the queries: [tile of 256 rows][32-deep k-block][256 rows][64 B]. A 32-deep k-step of a tile
+// is then one contiguous 16-KiB block whose 128-B lines are whole (row pairs), so the k-steps can
+// be 32 deep without splitting lines between two requests (the cost that sank 64-B half rows in
+// the row-major kernels), and 32-KiB stages leave room for a 4-stage ring: each k-step issues the
+// step 3 ahead (96 KiB in flight) right after its barrier and waits, with a counted vmcnt, only
+// for its own step — the t256 kernel's 64-deep 2-stage ring waited for the step it had just
+// issued. Bytes per MFMA are the t256 tile's (half the 128 x 128 kernels'). One barrier per 32
+// MFMAs per wave. The epilogue (group maxima, register stash, candidate buffer, fallback list,
+// end-of-kernel fold and lane-quarter merge) and the fragment map and k order are t256's, so the
+// scores and rows are bitwise those of t256 and of the small-batch kernel.
+// =============================================================================================
+namespace kb256 {
+constexpr int kTR = 256, kTQ = 256;
+constexpr int kKB = 64;                          // bytes of one row in one 32-deep k-block
+constexpr int kBlock = kTR * kKB;                // 16 KiB: one operand's k-step
+constexpr int kStage = 2 * kBlock;               // A (corpus) block, then B (queries) block
+constexpr int kStages = 4;
+constexpr int kLds = kStages * kStage;           // 128 KiB
+static_assert(kLds <= 160 * 1024, "kb256 LDS exceeds 160 KiB");
+// byte offset of (row, k-block) in a k-blocked buffer of n_kb k-blocks
+__host__ __device__ __forceinline__ int64_t offset(int64_t row, int kb, int n_kb) {
+  return (((row >> 8) * n_kb + kb) * kTR + (row & 255)) * kKB;
+}
+}  // namespace kb256
+
+// row-major storage rows [row0, row0 + n) -> k-blocked copy (one thread per 16-B chunk)
+__global__ __launch_bounds__(256) void reblock_kb_kernel(const uint8_t* __restrict__ src, int64_t row_stride,
+                                                         int64_t row0, int64_t n, int n_kb,
+                                                         uint8_t* __restrict__ dst) {
+  const int per_row = n_kb * 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * per_row) return;
+  const int64_t row = row0 + i / per_row;
+  const int ch = (int)(i % per_row);
+  const u32x4 v = *reinterpret_cast<const u32x4*>(src + row * row_stride + (int64_t)ch * 16);
+  *reinterpret_cast<u32x4*>(dst + kb256::offset(row, ch >> 2, n_kb) + (ch & 3) * 16) = v;
+}
+
+template <int DT, int KCAP>
+__global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
+    const uint8_t* __restrict__ corpus_kb, const uint8_t* __restrict__ queries_kb, int n_kb, int n_rows, int n_q,
+    int n_row_tiles, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
+    const float* __restrict__ thr_init, int n_splits, int qblocks, int flags, uint64_t* __restrict__ cand_keys,
+    int cand_cap) {
+  static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2;  // 128-row half of the tile
+  const int wn = wave & 3;   // 64-query quarter of the block
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  int split, qb;
+  if (flags & kFlagXcdRemap) {
+    const int x = blockIdx.x & 7;
+    const int i = blockIdx.x >> 3;
+    split = (i / qblocks) * 8 + x;
+    qb = i % qblocks;
+  } else {
+    split = blockIdx.x % n_splits;
+    qb = blockIdx.x / n_splits;
+  }
+  const int q0 = qb * kb256::kTQ;
+  const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
+  const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
+
+  float thr[4];
+  uint64_t thk[4];
+  int nc[4];
+  uint64_t stash[4];  // first survivor of a query slot (a store would hold the next vmcnt wait)
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int q = q0 + wn * 64 + nb * 16 + fr;
+    thr[nb] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+    thk[nb] = (q < n_q && thr[nb] != -INFINITY) ? (((uint64_t)ord_f32(thr[nb]) << 32) - 1) : 0;
+    nc[nb] = 0;
+    stash[nb] = 0;
+  }
+  auto cbase = [&](int nb) __attribute__((always_inline)) {
+    const int q = q0 + wn * 64 + nb * 16 + fr;
+    return ((int64_t)q * (8 * n_splits) + 8 * split + 4 * wm + fq) * cand_cap;
+  };
+  volatile uint64_t Ls[4][KCAP];  // private memory: touched only when a candidate buffer is full
+#pragma unroll 1
+  for (int j = 0; j < 4 * KCAP; ++j) Ls[j / KCAP][j % KCAP] = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thr_init reads retired before the ring counts
+
+  const int total = (t_end - t_begin) * n_kb;  // k-steps of this workgroup
+  if (total > 0) {
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    // DMA: per 16-KiB block, wave w fills rows [16w, 16w + 16) (j = 0) and [128 + 16w, ...) (j = 1),
+    // lane l at (row 16w + l/4, physical slot l%4), loading logical chunk (l%4) ^ ((row >> 2) & 3)
+    // (swz64): the 16 rows of a ds_read_b128 lane group then hit 16 distinct 16-B bank slots
+    const int lrow = wave_u * 16 + (lane >> 2);
+    const uint32_t voff = (uint32_t)(lrow * kb256::kKB + (((lane & 3) ^ ((lrow >> 2) & 3)) << 4));
+    const uint8_t* qblk = queries_kb + (int64_t)qb * n_kb * kb256::kBlock;
+    auto issue = [&](int c) __attribute__((always_inline)) {
+      const int t = t_begin + c / n_kb;
+      const int kb = c % n_kb;
+      const __amdgpu_buffer_rsrc_t a_rsrc =
+          tile_rsrc(corpus_kb + ((int64_t)t * n_kb + kb) * kb256::kBlock, kb256::kBlock);
+      const __amdgpu_buffer_rsrc_t b_rsrc = tile_rsrc(qblk + (int64_t)kb * kb256::kBlock, kb256::kBlock);
+      unsigned char* dst = smem + (c & (kb256::kStages - 1)) * kb256::kStage + wave_u * 16 * kb256::kKB;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (__attribute__((address_space(3))) void*)(dst + j * 8192),
+                                                 16, voff, j * 8192, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            b_rsrc, (__attribute__((address_space(3))) void*)(dst + kb256::kBlock + j * 8192), 16, voff, j * 8192, 0,
+            0);
+      }
+    };
+    // fragment reads: lane l reads row l & 15, logical chunk l / 16 (k 8(l/16) .. +8 of the step)
+    const uint32_t fo = (uint32_t)(fr * kb256::kKB + ((fq ^ ((fr >> 2) & 3)) << 4));
+
+    f32x4 acc[8][4];
+
+    auto list_push = [&](int nb, uint64_t key) {
+      int j = KCAP - 1;
+#pragma unroll 1
+      while (j > 0 && Ls[nb][j - 1] < key) {
+        Ls[nb][j] = Ls[nb][j - 1];
+        --j;
+      }
+      Ls[nb][j] = key;
+      const uint64_t kth = Ls[nb][k_out - 1];
+      if (kth > thk[nb]) {
+        thk[nb] = kth;
+        thr[nb] = key_score(kth);
+      }
+    };
+
+    const int pro = total < 3 ? total : 3;
+    for (int c = 0; c < pro; ++c) issue(c);
+    int t = t_begin;
+    int kb = 0;
+    for (int c = 0; c < total; ++c) {
+      // this wave's DMA of step c landed: leave the steps issued after it (up to 2) in flight
+      const int ahead = total - 1 - c;
+      if (!(flags & kFlagNoWait)) {
+        if (ahead >= 2)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (ahead == 1)
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lds_barrier();  // everyone's step c landed; everyone finished reading step c - 1
+      if (c + 3 < total && !((flags & kFlagNoLoads) && c >= 1)) issue(c + 3);  // into step c - 1's stage
+      if (kb == 0) {
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      const unsigned char* st = smem + (c & (kb256::kStages - 1)) * kb256::kStage;
+      const unsigned char* abase = st + (wm * 128) * kb256::kKB + fo;
+      const unsigned char* bbase = st + kb256::kBlock + (wn * 64) * kb256::kKB + fo;
+      u32x4 b[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const u32x4*>(bbase + nb * 16 * kb256::kKB);
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const u32x4 a = *reinterpret_cast<const u32x4*>(abase + mb * 16 * kb256::kKB);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) mfma16(a, b[nb], acc[mb][nb], DT);
+      }
+      if (++kb < n_kb) continue;
+      kb = 0;
+      const int tile = t++;
+      if (flags & kFlagSkipEpilogue) continue;
+      // ---- tile end: (query slot nb, row half mh) groups = acc[4 mh .. 4 mh + 3][nb], 16 rows
+      const int r0 = tile * kb256::kTR + wm * 128;
+      uint32_t gmask = 0;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+          float m = acc[4 * mh][nb][0];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) m = fmaxf(m, acc[4 * mh + u][nb][i]);
+          gmask |= (m >= thr[nb] ? 1u : 0u) << (nb * 2 + mh);
+        }
+      if (flags & kFlagMaxOnly) {  // ablation: group maxima only (wrong results)
+        if (gmask == 0xFFu && thr[0] == 1234.5f) part_keys[0] = 1;
+        continue;
+      }
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         const int nb = g >> 1, mh = g & 1;
@@ -2590,6 +2868,7 @@ using namespace ahr::dense;
 // One query workspace: converted queries, per-split partial lists, pre-pass scores/thresholds.
 struct ahr_query_ws {
   uint8_t* qbuf = nullptr;
+  uint8_t* qbuf_kb = nullptr;  // k-blocked copy of qbuf (half types: the kb256 kernel's B operand)
   int64_t q_cap = 0;
   uint64_t* part = nullptr;
   int64_t part_cap = 0;
@@ -2611,7 +2890,9 @@ struct ahr_index {
   int64_t row_stride = 0;
   int64_t count = 0;
   uint8_t* rows = nullptr;
+  uint8_t* rows_kb = nullptr;  // half types: k-blocked copy of rows (kb256::offset), kept in step by upsert
   uint8_t* qbuf = nullptr;
+  uint8_t* qbuf_kb = nullptr;
   int64_t q_cap = 0;  // rows in qbuf (multiple of kRowPad)
   uint64_t* part = nullptr;
   int64_t part_cap = 0;  // uint64 elements
@@ -2662,7 +2943,7 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 // 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed), 6 = 256x256 16x16x32
 // kernel (opt-in), 7 = small-batch streaming kernel (B <= 16; <= 64 opt-in)
 enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
-       KERNEL_T256 = 6, KERNEL_SMALL = 7 };
+       KERNEL_T256 = 6, KERNEL_SMALL = 7, KERNEL_KB256 = 8 };
 
 struct SearchPlan {
   int kernel;
@@ -2712,6 +2993,14 @@ bool small_ok(const ahr_index* ix, int B, int k) {
   return small::lds_bytes(ix->row_stride, 16, small::groups(B)) <= 160 * 1024;
 }
 
+// The k-blocked 256x256 kernel: half types (the k-blocked corpus copy exists), k <= 16; opt-in
+// (kFlagKB256) until it is measured ahead of the plans below.
+bool kb256_ok(const ahr_index* ix, int B, int k) {
+  if (k > 16 || ix->dtype == AHR_F32 || !ix->rows_kb) return false;
+  if (ix->debug_flags & kFlagNoKB256) return false;
+  return (ix->debug_flags & kFlagKB256) != 0 && B > 0;
+}
+
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
@@ -2732,6 +3021,18 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.kernel = KERNEL_T256;
     p.qblocks = (int)cdiv(B, t256::kTQ);
     p.n_row_tiles = (int)cdiv(ix->count, t256::kTR);
+    int want = std::max(1, 256 / p.qblocks);
+    want = std::min(want, std::max(1, p.n_row_tiles));
+    p.xcd_remap = want >= 8;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    return p;
+  }
+  if (kb256_ok(ix, B, k)) {
+    // 256x256 tiles, one workgroup per CU: one wave of 256 workgroups
+    p.kernel = KERNEL_KB256;
+    p.qblocks = (int)cdiv(B, kb256::kTQ);
+    p.n_row_tiles = (int)cdiv(ix->count, kb256::kTR);
     int want = std::max(1, 256 / p.qblocks);
     want = std::min(want, std::max(1, p.n_row_tiles));
     p.xcd_remap = want >= 8;
@@ -2796,11 +3097,17 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
   const int64_t q_need = cdiv(B, kRowPad) * kRowPad;
   if (q_need > ix->q_cap) {
     if (ix->qbuf) AHR_HIP(hipFree(ix->qbuf));
-    ix->qbuf = nullptr;
+    if (ix->qbuf_kb) AHR_HIP(hipFree(ix->qbuf_kb));
+    ix->qbuf = ix->qbuf_kb = nullptr;
     ix->q_cap = 0;
     if (hipMalloc(&ix->qbuf, q_need * ix->row_stride) != hipSuccess)
       return fail(AHR_ENOMEM, "query workspace allocation failed");
     AHR_HIP(hipMemsetAsync(ix->qbuf, 0, q_need * ix->row_stride, s));
+    if (ix->rows_kb) {
+      if (hipMalloc(&ix->qbuf_kb, q_need * ix->row_stride) != hipSuccess)
+        return fail(AHR_ENOMEM, "query workspace allocation failed");
+      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, q_need * ix->row_stride, s));
+    }
     ix->q_cap = q_need;
   }
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
@@ -2876,7 +3183,7 @@ void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B
 // lane's private list inside the kernel, so the cap only trades memory for speed.
 inline int qkv_cand_cap(const SearchPlan& p) { return (int)std::min(64, std::max(16, p.tiles_per_split)); }
 inline int64_t cand_bytes(int B, const SearchPlan& p) {
-  const int64_t prod = p.kernel == KERNEL_T256 ? 8 : 4;  // candidate producers per (query, split)
+  const int64_t prod = (p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) ? 8 : 4;  // producers per (query, split)
   return (int64_t)B * prod * p.n_splits * qkv_cand_cap(p) * 8;
 }
 
@@ -2910,6 +3217,17 @@ void launch_t256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), t256::kLds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), t256::kLds, s, ix->rows, ix->qbuf,
                      ix->row_stride, n_rows, B, ix->d_pad * ix->elem / kRowBytes, p.n_row_tiles, row_base, k, ix->part,
+                     thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
+}
+
+template <int DT, int KCAP>
+void launch_kb256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
+                  const float* thr, int flags, hipStream_t s) {
+  constexpr auto kern = &topk_kb256_kernel<DT, KCAP>;
+  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), kb256::kLds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), kb256::kLds, s, ix->rows_kb,
+                     ix->qbuf_kb, ix->d_pad * ix->elem / kb256::kKB, n_rows, B, p.n_row_tiles, row_base, k, ix->part,
                      thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
 
@@ -3018,6 +3336,15 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
+    if (p.kernel == KERNEL_KB256) {
+      if (k <= 8)
+        launch_kb256<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s);
+      else if (k <= 12)
+        launch_kb256<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s);
+      else
+        launch_kb256<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s);
+      return;
+    }
     if (p.kernel == KERNEL_T256) {
       if (k <= 8)
         launch_t256<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s);
@@ -3160,9 +3487,15 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     }
   }
   SearchPlan p = plan_search(ix, B, k);
-  if ((p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256) && ix->count > 0) {
+  if ((p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) && ix->count > 0) {
     st = ensure_cand(ix, cand_bytes(B, p));
     if (st) return st;
+  }
+  if (p.kernel == KERNEL_KB256 && ix->count > 0) {
+    const int n_kb = ix->d_pad * ix->elem / kb256::kKB;
+    const int64_t chunks = (int64_t)B * n_kb * 4;
+    hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->qbuf,
+                       ix->row_stride, (int64_t)0, (int64_t)B, n_kb, ix->qbuf_kb);
   }
   if (ix->count > 0) {
     switch (ix->dtype) {
@@ -3176,8 +3509,9 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   }
   prof_mark(ix, 3, s);
   {
-    // qkv: one list per (split, dimension half); t256: one per (split, row half)
-    const int lists = (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 ? 2 : 1) * p.n_splits;
+    // qkv: one list per (split, dimension half); t256 / kb256: one per (split, row half)
+    const int lists = (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256 ? 2 : 1) *
+                      p.n_splits;
     launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
   }
   prof_mark(ix, 4, s);
@@ -3211,9 +3545,18 @@ int ahr_index_create(int dim, int dtype, int64_t capacity, int device, ahr_index
     delete ix;
     return fail(AHR_ENOMEM, "corpus allocation failed");
   }
-  // zeroed before any stream (also non-blocking ones) writes rows into it
-  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+  // half types keep a k-blocked copy for the kb256 kernel (same bytes; 288 GB of HBM affords it)
+  if (dtype != AHR_F32 && hipMalloc(&ix->rows_kb, ix->cap_pad * ix->row_stride) != hipSuccess) {
     (void)hipFree(ix->rows);
+    delete ix;
+    return fail(AHR_ENOMEM, "corpus allocation failed");
+  }
+  // zeroed before any stream (also non-blocking ones) writes rows into it
+  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess ||
+      (ix->rows_kb && hipMemset(ix->rows_kb, 0, ix->cap_pad * ix->row_stride) != hipSuccess) ||
+      hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(ix->rows);
+    if (ix->rows_kb) (void)hipFree(ix->rows_kb);
     delete ix;
     return fail(AHR_EHIP, "corpus memset failed");
   }
@@ -3225,13 +3568,16 @@ int ahr_index_destroy(ahr_index* ix) {
   if (!ix) return AHR_OK;
   DeviceGuard dg(ix->device);
   if (ix->rows) (void)hipFree(ix->rows);
+  if (ix->rows_kb) (void)hipFree(ix->rows_kb);
   if (ix->qbuf) (void)hipFree(ix->qbuf);
+  if (ix->qbuf_kb) (void)hipFree(ix->qbuf_kb);
   if (ix->part) (void)hipFree(ix->part);
   if (ix->sample) (void)hipFree(ix->sample);
   if (ix->cand) (void)hipFree(ix->cand);
   for (int w = 0; w < kMaxWorkspaces; ++w) {
     if (w == ix->cur_ws) continue;
     if (ix->parked[w].qbuf) (void)hipFree(ix->parked[w].qbuf);
+    if (ix->parked[w].qbuf_kb) (void)hipFree(ix->parked[w].qbuf_kb);
     if (ix->parked[w].part) (void)hipFree(ix->parked[w].part);
     if (ix->parked[w].sample) (void)hipFree(ix->parked[w].sample);
     if (ix->parked[w].cand) (void)hipFree(ix->parked[w].cand);
@@ -3275,6 +3621,14 @@ int ahr_index_upsert(ahr_index* ix, const float* vecs, int64_t n, const int64_t*
   hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s, vecs, n,
                      ix->dim, slots, start_slot, normalize, ix->rows, ix->row_stride, ix->d_pad,
                      ix->dtype);
+  if (ix->rows_kb) {
+    // the k-blocked copy of the rows just written (scattered slots: every row below the highest)
+    const int64_t lo = slots ? 0 : start_slot;
+    const int n_kb = ix->d_pad * ix->elem / kb256::kKB;
+    const int64_t chunks = (hi - lo) * n_kb * 4;
+    hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->rows,
+                       ix->row_stride, lo, hi - lo, n_kb, ix->rows_kb);
+  }
   AHR_HIP(hipGetLastError());
   ix->count = std::max(ix->count, hi);
   return AHR_OK;
@@ -3378,6 +3732,7 @@ int ahr_index_set_workspace(ahr_index* ix, int slot) {
   if (slot == ix->cur_ws) return AHR_OK;
   ahr_query_ws& out = ix->parked[ix->cur_ws];
   out.qbuf = ix->qbuf;
+  out.qbuf_kb = ix->qbuf_kb;
   out.q_cap = ix->q_cap;
   out.part = ix->part;
   out.part_cap = ix->part_cap;
@@ -3387,6 +3742,7 @@ int ahr_index_set_workspace(ahr_index* ix, int slot) {
   out.cand_cap = ix->cand_cap;
   ahr_query_ws& in = ix->parked[slot];
   ix->qbuf = in.qbuf;
+  ix->qbuf_kb = in.qbuf_kb;
   ix->q_cap = in.q_cap;
   ix->part = in.part;
   ix->part_cap = in.part_cap;
@@ -3419,7 +3775,7 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
   // candidate groups of the query-resident plan at the current corpus size
   for (int kk = 1; kk <= max_k; kk = kk < 8 ? 8 : kk + 8) {
     const SearchPlan p = plan_search(ix, max_batch, kk);
-    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256) {
+    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) {
       st = ensure_cand(ix, cand_bytes(max_batch, p));
       if (st) return st;
     }

@@ -437,6 +437,60 @@ def test_t256_matches_tilelane(cuda, dtype, n, d, B, k, sample):
     _close_topk(a, b)
 
 
+# ---- k-blocked 256 x 256 kernel (kb256): bitwise the t256 kernel's scores and rows ------------------------------
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n,d,B,k,sample", [
+    (40001, 768, 1024, 10, 8192), (40001, 768, 1024, 10, 0), (33000, 384, 300, 16, 8192),
+    (300, 768, 1, 1, 0), (1000, 128, 257, 8, 0), (90000, 768, 2048, 5, 8192), (5000, 100, 17, 12, 0),
+    (4000, 1100, 40, 10, 0), (90000, 768, 1024, 10, 8192)])
+def test_kb256_matches_t256(cuda, dtype, n, d, B, k, sample):
+    """Same 16x16x32 fragment map and k order as t256 (only the staging differs: 32-deep k-blocked
+    steps through a 4-stage ring): scores and rows bitwise equal; ragged last tile, splits without
+    tiles, d_pad 128 / 1152, no seed."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(191 + n + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    half = n // 2 + 37  # two upserts: the k-blocked copy is refreshed per written range
+    ix.upsert(C[:half])
+    ix.upsert(C[half:], start=half)
+    ix.set_sample_rows(sample)
+    ix.set_debug_flags(131072)
+    assert ix.plan(B, k)["kernel"] == "kb256"
+    a = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(32768)
+    assert ix.plan(B, k)["kernel"] == "t256"
+    b = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.close()
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0], b[0])
+    kk = min(k, n)
+    Cr, Qr = dr.round_to_storage(C, dtype), dr.round_to_storage(Q, dtype)
+    es, _ = dr.topk(Cr, Qr, k, mode="f64")
+    assert np.abs(a[0][:, :kk] - es[:, :kk]).max() < 1e-4
+
+
+def test_kb256_slot_upsert_and_ties(cuda):
+    """Scattered-slot upserts refresh the k-blocked copy; duplicate rows order by row id."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(23)
+    base = _clustered(rng, 300, 768)
+    C = np.concatenate([base] * 40)  # 12000 rows, each vector 40 times
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(np.zeros_like(C))
+    perm = rng.permutation(len(C))
+    ix.upsert(C[perm], slots=perm)
+    ix.set_debug_flags(131072)
+    pick = rng.integers(0, 300, 64)
+    assert ix.plan(64, 16)["kernel"] == "kb256"
+    s, r = [t.cpu().numpy() for t in ix.query(base[pick], 16)]
+    ix.close()
+    np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(16)[None, :])
+    assert (s == s[:, :1]).all()
+
+
 # ---- small batches (B <= 16; <= 64 opt-in, bf16/f16, k <= 16): corpus-streaming 16x16x32 kernel -------------
 
 def test_small_plans(cuda):
