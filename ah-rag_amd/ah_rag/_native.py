@@ -52,9 +52,9 @@ EXPORTED_SYMBOLS = (
     "ahr_index_count", "ahr_index_info", "ahr_index_rows", "ahr_index_read", "ahr_index_reserve",
     "ahr_index_profile_begin", "ahr_index_profile_end", "ahr_index_set_sample_rows", "ahr_index_plan",
     "ahr_index_set_debug_flags", "ahr_index_set_workspace",
-    "ahr_index_query", "ahr_index_query_keys", "ahr_topk_merge", "ahr_key_decode",
+    "ahr_index_query", "ahr_index_query_keys", "ahr_index_scores", "ahr_topk_merge", "ahr_key_decode",
     "ahr_graph_create", "ahr_graph_destroy", "ahr_graph_expand_rerank", "ahr_graph_expand",
-    "ahr_graph_info",
+    "ahr_graph_lca", "ahr_graph_info",
 )
 
 
@@ -103,6 +103,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_index_set_debug_flags": ([_P, _I], _I),
         "ahr_index_query": ([_P, _P, _I, _I, _I, _P, _P, _P], _I),
         "ahr_index_query_keys": ([_P, _P, _I, _I, _I, _L, _P, _P], _I),
+        "ahr_index_scores": ([_P, _P, _I, _I, _P, _L, _P], _I),
         "ahr_topk_merge": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
         "ahr_key_decode": ([_P, _L, _P, _P], _I),
         "ahr_graph_create": ([_L, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
@@ -110,6 +111,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_graph_expand_rerank": ([_P, _P, _P, _I, _I, ctypes.POINTER(RerankParams), _I,
                                      _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
         "ahr_graph_expand": ([_P, _I, _P, _I, _I, _I, _P, _P, _P], _I),
+        "ahr_graph_lca": ([_P, _P, _I, _I, _I, _P, _P, _P], _I),
         "ahr_graph_info": ([_P, _P, _P], _I),
     }
     for name, (args, res) in sig.items():

@@ -207,34 +207,15 @@ class GraphEnvironment:
             self._dag_cache = (stamp, seen == len(members), {dg.ids[i] for i in members})
         return self._dag_cache[1], self._dag_cache[2]
 
-    def _ancestors_or_self(self, node_id: str) -> Set[str]:
-        """Nodes with a belongs_to path TO node_id, plus itself (nx.ancestors on the belongs_to DAG)."""
-        dg = self.hg.device_graph()
-        start = dg.index[node_id]
-        seen = {start}
-        stack = [start]
-        while stack:
-            u = stack.pop()
-            for v in dg.neighbors(u, ADJ_BT_IN):
-                v = int(v)
-                if v not in seen:
-                    seen.add(v)
-                    stack.append(v)
-        return {dg.ids[i] for i in seen}
-
     def expand_to_lca(self, node_ids: List[str], max_results: int = 5) -> Tuple[Dict[str, Any], Dict[str, Any]]:
         self._ensure_graph_loaded()
         self.step_count += 1
         is_dag, dag_nodes = self._belongs_to_dag()
-        sets = []
         for nid in node_ids:
             if nid not in dag_nodes:
                 raise nx.NetworkXError(f"The node {nid} is not in the digraph.")
-            sets.append(self._ancestors_or_self(nid))
-        inter = set.intersection(*sets) if sets else set()
+        lowest = lca_batch(self.hg, [node_ids])[0]  # ancestor sets + intersection on the device
         G = self.hg.G
-        lowest = [n for n in inter
-                  if not any(a.get("edge_type") == "belongs_to" and v in inter for v, a in G.succ[n].items())]
         t0 = time.perf_counter()
         picked = sorted(lowest, key=lambda x: (G.nodes[x].get("level") or 1, x))[:max_results]
         obs = self._observation([{"node_id": n, "semantic": 0.0} for n in picked],
@@ -346,6 +327,23 @@ class GraphEnvironment:
             pass
         self._log({"action": "end_episode"})
         return summary
+
+
+def lca_batch(hg: HierarchicalGraph, inputs: Sequence[Sequence[str]]) -> List[List[str]]:
+    """Lowest common members of each input list on the belongs_to DAG, one ahr_graph_lca launch for
+    the batch (environment.py:243-289 before the (level, id) sort). The ids must be DAG nodes."""
+    dg = hg.device_graph()
+    width = max(1, max((len(x) for x in inputs), default=1))
+    idx = np.full((len(inputs), width), -1, np.int32)
+    for b, ids in enumerate(inputs):
+        if ids:
+            idx[b, :len(ids)] = dg.node_indices(ids)
+    out, cnt = dg.lca(torch.from_numpy(idx))
+    out_h, cnt_h = out.cpu().numpy(), cnt.cpu().numpy()
+    if (cnt_h < 0).any():
+        raise RuntimeError("expand_to_lca: an ancestor set exceeds the device kernel's capacity "
+                           "(4096 nodes, 1024 per level; include/ahr.h ahr_graph_lca)")
+    return [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] for b in range(len(inputs))]
 
 
 def expand_batch(hg: HierarchicalGraph, action: str, inputs: Sequence[Sequence[str]], limit: int = 10

@@ -7,7 +7,8 @@ thresholds (:640-646), weight 0.5·jaccard + 0.5·cosine (:649), rounded fields 
 top-k by weight (:664-665), then artifacts/l1_edges.json, a `neighbors` list on every node and
 artifacts/l1_nodes.json (:667-680).
 
-Here the O(T²·d) part is one GEMM on the GPU (the centroid cosine matrix, fp32, library GEMM),
+Here the O(T²·d) part is one pass of this library's fp32 tile kernel (ahr_index_scores: the
+centroid cosine matrix),
 member overlaps are one sparse product of the topic × member incidence matrix, and only the pairs
 that pass a rule reach the host loop, which keeps the reference's arithmetic (Python floats,
 round()) and pair order (sorted topic ids, row-major upper triangle).
@@ -59,8 +60,10 @@ def overlap_matrix(topic_ids: Sequence[int], members: Dict[int, set]) -> np.ndar
 
 def cosine_matrix_gpu(topic_ids: Sequence[int], centroids: Dict[int, Optional[np.ndarray]],
                       device: Optional[torch.device] = None) -> np.ndarray:
-    """float32 cosine of every centroid pair: one fp32 GEMM on the GPU. Missing centroids give 0
-    (reference :636-638). Raises without a GPU (no CPU fallback in the product path)."""
+    """float32 cosine of every centroid pair in one device pass: the centroids become an fp32
+    DenseIndex and ahr_index_scores runs the fused tile kernel's GEMM core over them (every score
+    a k-ordered fma chain). Missing centroids give 0 (reference :636-638). Raises without a GPU
+    (no CPU fallback in the product path)."""
     if not torch.cuda.is_available():
         raise RuntimeError("generate_l1_relations needs a GPU (HIP device) for the centroid GEMM")
     dev = device or torch.device("cuda", torch.cuda.current_device())
@@ -73,8 +76,13 @@ def cosine_matrix_gpu(topic_ids: Sequence[int], centroids: Dict[int, Optional[np
         c = centroids.get(t)
         if c is not None:
             X[i] = c
-    x = torch.from_numpy(X).to(dev)
-    return torch.mm(x, x.T).cpu().numpy()
+    from ..embeddings import DenseIndex
+    ix = DenseIndex(d, max(1, len(topic_ids)), dtype="f32", device=dev)
+    try:
+        ix.upsert(X)
+        return ix.scores(X).cpu().numpy()  # fp32 tile kernel, scores mode (ahr_index_scores)
+    finally:
+        ix.close()
 
 
 def edges_from_matrices(topic_ids: Sequence[int], members: Dict[int, set], confidences: Dict[int, float],

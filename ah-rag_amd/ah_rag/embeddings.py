@@ -260,6 +260,19 @@ class DenseIndex:
                       "ahr_index_query")
         return scores, rows
 
+    def scores(self, queries: ArrayLike, normalize: bool = False,
+               stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+        """Every score [B, count] fp32 on the device (ahr_index_scores: the tile kernel's GEMM core
+        in scores mode; fp32 index = k-ordered fma chains)."""
+        q = _as_f32_device(queries, self.device)
+        n = len(self)
+        out = torch.empty((q.shape[0], max(n, 1)), dtype=torch.float32, device=self.device)
+        _on_stream(stream, self.device, q, out)
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_scores(self._h, nat.ptr(q), q.shape[0], int(bool(normalize)), nat.ptr(out),
+                                                 out.shape[1], nat.stream_ptr(stream)), "ahr_index_scores")
+        return out[:, :n]
+
     def query_keys(self, queries: ArrayLike, k: int, row_base: int = 0, normalize: bool = False,
                    stream: Optional[torch.cuda.Stream] = None,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:

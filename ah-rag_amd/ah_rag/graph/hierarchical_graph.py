@@ -97,11 +97,86 @@ class VectorStore:
             json.dump({"model": model, "ids": self.ids, "metadatas": self.metas}, f, ensure_ascii=False)
 
     def stamp(self) -> Tuple:
-        try:
-            st = os.stat(os.path.join(self.path, VECTORS_FILE))
-            return (st.st_mtime_ns, st.st_size)
-        except OSError:
-            return (0, 0)
+        return store_stamp(self.path)
+
+
+def store_stamp(path: str) -> Tuple:
+    """(mtime, size) of a store's vector file: a change made by another writer forces a reload."""
+    try:
+        st = os.stat(os.path.join(path, VECTORS_FILE))
+        return (st.st_mtime_ns, st.st_size)
+    except OSError:
+        return (0, 0)
+
+
+class ResidentIndex:
+    """The HBM copy of one vector store (Chroma's collection role): DenseIndex + row id table.
+
+    build_vector_index writes it incrementally — rows whose sha1 key changed are upserted into
+    their slots, new nodes appended (ahr_index_upsert), the reference's collection semantics
+    (hierarchical_graph.py:660: existing ids updated in place, new ids appended in order) — so a
+    re-index after editing a few nodes moves those rows only, never the whole store."""
+
+    def __init__(self, path: str, device) -> None:
+        self.path = path
+        self.device = device
+        self.dtype = os.environ.get("AHR_INDEX_DTYPE", "f32")
+        self.full_loads = 0
+        self.rows_upserted = 0
+        self.version = 0
+        self.index: Optional[DenseIndex] = None
+        self.reload()
+
+    def reload(self) -> None:
+        store = VectorStore(self.path)
+        n, dim = store.vectors.shape if store.vectors.size else (0, 1)
+        self._alloc(dim, max(n, 1))
+        if n:
+            self.index.upsert(store.vectors)
+        self.ids, self.metas = list(store.ids), list(store.metas)
+        self.slot = {nid: i for i, nid in enumerate(self.ids)}
+        self.stamp = store.stamp()
+        self.full_loads += 1
+        self.version += 1
+
+    def _alloc(self, dim: int, capacity: int) -> None:
+        if self.index is not None:
+            self.index.close()
+        # headroom so that appended nodes rarely force a reallocation
+        self.index = DenseIndex(dim, capacity + max(256, capacity // 4), dtype=self.dtype, device=self.device)
+
+    def apply(self, ids: Sequence[str], vectors: np.ndarray, metas: Sequence[Dict[str, Any]]) -> None:
+        """Upsert rows into the resident index in the store's slot order (VectorStore.upsert)."""
+        if vectors.shape[1] != self.index.dim:
+            self.reload()
+            return
+        old_i, old_s, new_i = [], [], []
+        for i, nid in enumerate(ids):
+            if nid in self.slot:
+                old_i.append(i)
+                old_s.append(self.slot[nid])
+                self.metas[self.slot[nid]] = dict(metas[i])
+            else:
+                new_i.append(i)
+        n0 = len(self.ids)
+        if n0 + len(new_i) > self.index.capacity:
+            self.reload()  # grow: one full upload of the (already saved) store
+            return
+        if old_i:
+            self.index.upsert(vectors[old_i], slots=np.asarray(old_s, np.int64))
+        if new_i:
+            self.index.upsert(vectors[new_i], start=n0)
+            for i in new_i:
+                self.slot[ids[i]] = len(self.ids)
+                self.ids.append(ids[i])
+                self.metas.append(dict(metas[i]))
+        self.rows_upserted += len(old_i) + len(new_i)
+        self.stamp = store_stamp(self.path)
+        self.version += 1
+
+    def close(self) -> None:
+        if self.index is not None:
+            self.index.close()
 
 
 class HierarchicalGraph:
@@ -119,6 +194,7 @@ class HierarchicalGraph:
                                                  "indexed_nodes": 0, "indexed_meta": {}})
         self._version = 0
         self._dev_graph: Optional[Tuple[Tuple, DeviceGraph]] = None
+        self._indexes: Dict[str, ResidentIndex] = {}
         self._engines: Dict[str, Tuple[Tuple, SearchEngine]] = {}
 
     # ---- ids ---------------------------------------------------------------------------------
@@ -519,6 +595,14 @@ class HierarchicalGraph:
                                                              normalize_embeddings=True), np.float32)
         store.upsert(todo, vectors, metas)
         store.save(model_name)
+        # the resident HBM copy follows the same upsert (changed rows only); a reset drops it
+        resident = self._indexes.get(os.path.abspath(db_path))
+        if resident is not None:
+            if reset:
+                resident.close()
+                self._indexes.pop(os.path.abspath(db_path))
+            else:
+                resident.apply(todo, vectors, metas)
         new_meta = dict(prev)
         for nid in todo:
             new_meta[nid] = self._index_key(self.G.nodes[nid])
@@ -537,21 +621,25 @@ class HierarchicalGraph:
             self._engines.clear()
         return self._dev_graph[1]
 
+    def resident_index(self, db_path: str) -> ResidentIndex:
+        """The store at db_path resident in HBM; reloaded whole only when another writer changed
+        the file (build_vector_index keeps it current incrementally)."""
+        key = os.path.abspath(db_path)
+        res = self._indexes.get(key)
+        if res is None:
+            res = self._indexes[key] = ResidentIndex(key, self.device_graph().device)
+        elif res.stamp != store_stamp(key):
+            res.reload()
+        return res
+
     def search_engine(self, db_path: str) -> SearchEngine:
         graph = self.device_graph()
         key = os.path.abspath(db_path)
-        store_stamp = VectorStore.__new__(VectorStore)
-        store_stamp.path = key
-        stamp = store_stamp.stamp()
+        res = self.resident_index(key)
+        stamp = (id(res), res.version, id(graph))
         hit = self._engines.get(key)
         if hit is None or hit[0] != stamp:
-            store = VectorStore(key)
-            n, dim = store.vectors.shape if store.vectors.size else (0, 1)
-            index = DenseIndex(dim, max(n, 1), dtype=os.environ.get("AHR_INDEX_DTYPE", "f32"),
-                               device=graph.device)
-            if n:
-                index.upsert(store.vectors)
-            self._engines[key] = (stamp, SearchEngine(index, store.ids, store.metas, graph))
+            self._engines[key] = (stamp, SearchEngine(res.index, res.ids, res.metas, graph))
         return self._engines[key][1]
 
     def _encoder(self, model_name: str):

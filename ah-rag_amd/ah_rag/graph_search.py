@@ -176,6 +176,22 @@ class DeviceGraph:
                 nat.ptr(osc), nat.ptr(oc), nat.stream_ptr(stream)), "ahr_graph_expand_rerank")
         return RerankResult(en, es, ex, ec, on, osem, osc, oc)
 
+    def lca(self, inputs: torch.Tensor, max_out: int = 1024,
+            stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Batched expand_to_lca core (ahr_graph_lca): inputs int32 [B, n_in] node indices ->
+        (out int32 [B, max_out] unordered lowest common members, count int32 [B]; -1 = over the
+        kernel's per-query capacity)."""
+        B, n_in = inputs.shape
+        dev = self.device
+        out = torch.empty((B, max(max_out, 1)), dtype=torch.int32, device=dev)
+        cnt = torch.empty((B,), dtype=torch.int32, device=dev)
+        x = inputs.to(device=dev, dtype=torch.int32).contiguous()
+        _on_stream(stream, dev, x, out, cnt)
+        with torch.cuda.device(dev):
+            nat.check(nat.lib().ahr_graph_lca(self._h, nat.ptr(x), B, n_in, int(max_out), nat.ptr(out), nat.ptr(cnt),
+                                              nat.stream_ptr(stream)), "ahr_graph_lca")
+        return out, cnt
+
     def expand(self, action: str, inputs: torch.Tensor, limit: int = 10,
                stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Batched environment expansion: inputs int32 [B, n_in] node indices (-1 = skip)."""

@@ -33,6 +33,7 @@
 #include "ahr.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <math.h>
 #include <vector>
 
@@ -1428,6 +1429,13 @@ static_assert(kLds <= 160 * 1024, "kb256 LDS exceeds 160 KiB");
 __host__ __device__ __forceinline__ int64_t offset(int64_t row, int kb, int n_kb) {
   return (((row >> 8) * n_kb + kb) * kTR + (row & 255)) * kKB;
 }
+// LDS image of a 64-B row: logical 16-B chunk c of row r sits in physical slot c ^ h(r), h(r) =
+// (-(r >> 2)) & 3. A 256-B bank row holds 4 rows; a ds_read_b128 lane group of the 16x16x32
+// fragment reads rows 0-3 and 12-15 at chunk q and rows 4-11 at chunk q ^ 1 (lanes {0-3, 12-15,
+// 20-27}), so the rows r = i, i + 4, i + 8, i + 12 of a group need distinct slots: h(0..3) =
+// 0, 3, 2, 1 makes {h0, 1 ^ h1, 1 ^ h2, h3} = {0, 2, 3, 1} (and its XOR with 1, 2, 3 for the
+// other groups) a permutation: conflict-free. (The plain c ^ ((r >> 2) & 3) is 2-way.)
+__host__ __device__ __forceinline__ int phys(int chunk, int row) { return chunk ^ ((-(row >> 2)) & 3); }
 }  // namespace kb256
 
 // row-major storage rows [row0, row0 + n) -> k-blocked copy (one thread per 16-B chunk)
@@ -1472,16 +1480,16 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
   const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
   const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
 
+  // Per query slot: the admission threshold (a score: every score >= it is a candidate; the seed
+  // is a lower bound of the final k-th best), the first survivor in a register (a store would hold
+  // the next vmcnt wait) and the candidate-buffer fill, 8 bits per slot in one register.
   float thr[4];
-  uint64_t thk[4];
-  int nc[4];
-  uint64_t stash[4];  // first survivor of a query slot (a store would hold the next vmcnt wait)
+  uint64_t stash[4];
+  uint32_t ncp = 0;
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb) {
     const int q = q0 + wn * 64 + nb * 16 + fr;
     thr[nb] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
-    thk[nb] = (q < n_q && thr[nb] != -INFINITY) ? (((uint64_t)ord_f32(thr[nb]) << 32) - 1) : 0;
-    nc[nb] = 0;
     stash[nb] = 0;
   }
   auto cbase = [&](int nb) __attribute__((always_inline)) {
@@ -1497,10 +1505,11 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
   if (total > 0) {
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     // DMA: per 16-KiB block, wave w fills rows [16w, 16w + 16) (j = 0) and [128 + 16w, ...) (j = 1),
-    // lane l at (row 16w + l/4, physical slot l%4), loading logical chunk (l%4) ^ ((row >> 2) & 3)
-    // (swz64): the 16 rows of a ds_read_b128 lane group then hit 16 distinct 16-B bank slots
+    // lane l at (row 16w + l/4, physical slot l%4), loading the logical chunk whose kb256::phys is
+    // l%4 (phys is an involution in the chunk): every ds_read_b128 lane group hits 16 distinct
+    // 16-B bank slots
     const int lrow = wave_u * 16 + (lane >> 2);
-    const uint32_t voff = (uint32_t)(lrow * kb256::kKB + (((lane & 3) ^ ((lrow >> 2) & 3)) << 4));
+    const uint32_t voff = (uint32_t)(lrow * kb256::kKB + (kb256::phys(lane & 3, lrow) << 4));
     const uint8_t* qblk = queries_kb + (int64_t)qb * n_kb * kb256::kBlock;
     auto issue = [&](int c) __attribute__((always_inline)) {
       const int t = t_begin + c / n_kb;
@@ -1519,7 +1528,7 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
       }
     };
     // fragment reads: lane l reads row l & 15, logical chunk l / 16 (k 8(l/16) .. +8 of the step)
-    const uint32_t fo = (uint32_t)(fr * kb256::kKB + ((fq ^ ((fr >> 2) & 3)) << 4));
+    const uint32_t fo = (uint32_t)(fr * kb256::kKB + (kb256::phys(fq, fr) << 4));
 
     f32x4 acc[8][4];
 
@@ -1532,10 +1541,7 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
       }
       Ls[nb][j] = key;
       const uint64_t kth = Ls[nb][k_out - 1];
-      if (kth > thk[nb]) {
-        thk[nb] = kth;
-        thr[nb] = key_score(kth);
-      }
+      if (kth) thr[nb] = fmaxf(thr[nb], key_score(kth));
     };
 
     const int pro = total < 3 ? total : 3;
@@ -1614,15 +1620,14 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
 #pragma unroll
             for (int rr = 1; rr < 16; ++rr) v = (r == rr) ? acc[4 * mh + (rr >> 2)][nb][rr & 3] : v;
             const uint64_t key = make_key(v, row_base + (uint32_t)(rb + 16 * (r >> 2) + (r & 3)));
-            if (key > thk[nb]) {
-              if (stash[nb] == 0) {
-                stash[nb] = key;
-              } else if (nc[nb] < cand_cap) {
-                cand_keys[cbase(nb) + nc[nb]] = key;
-                ++nc[nb];
-              } else {
-                list_push(nb, key);
-              }
+            const int n = (ncp >> (8 * nb)) & 255;
+            if (stash[nb] == 0) {
+              stash[nb] = key;
+            } else if (n < cand_cap) {
+              cand_keys[cbase(nb) + n] = key;
+              ncp += 1u << (8 * nb);
+            } else {
+              list_push(nb, key);
             }
           }
         }
@@ -1649,7 +1654,7 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
 #pragma unroll
     for (int j = 0; j < KCAP; ++j) L[j] = Ls[nb][j];
     if (stash[nb]) list_insert<KCAP>(L, stash[nb]);
-    const int n = nc[nb];
+    const int n = (ncp >> (8 * nb)) & 255;
     const int64_t cb = q < n_q ? cbase(nb) : 0;
     for (int g0 = 0; g0 < n; g0 += 8) {
       uint64_t c8[8];
@@ -3794,6 +3799,38 @@ int ahr_index_query_keys(ahr_index* ix, const float* q, int B, int k, int normal
                          int64_t row_base, uint64_t* keys, void* stream) {
   if (!keys) return fail(AHR_EINVAL, "null output");
   return run_query(ix, q, B, k, normalize_q, row_base, nullptr, nullptr, keys, stream);
+}
+
+int ahr_index_scores(ahr_index* ix, const float* q, int B, int normalize_q, float* out, int64_t ld, void* stream) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (B < 0) return fail(AHR_EINVAL, "B must be >= 0");
+  if (ld < ix->count) return fail(AHR_EINVAL, "ld must be >= the row count");
+  if (B == 0 || ix->count == 0) return AHR_OK;
+  if (!q || !out) return fail(AHR_EINVAL, "null buffer");
+  DeviceGuard dg(ix->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int st = ensure_query_ws(ix, B, 1, s);
+  if (st) return st;
+  hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B, ix->dim,
+                     (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad,
+                     ix->dtype);
+  const int n = (int)ix->count;
+  const int n_row_tiles = (int)cdiv(n, kTileRows);
+  const int qblocks = (int)cdiv(B, kTileQ);
+  const int n_splits = std::max(1, std::min(n_row_tiles, kResidentSlots128 / qblocks));
+  switch (ix->dtype) {
+    case AHR_BF16:
+      launch_tile<DT_BF16, 8, MODE_SCORES>(ix, n_splits, qblocks, 1, n_row_tiles, n, B, 1, 0, nullptr, out, ld, 0, s);
+      break;
+    case AHR_F16:
+      launch_tile<DT_F16, 8, MODE_SCORES>(ix, n_splits, qblocks, 1, n_row_tiles, n, B, 1, 0, nullptr, out, ld, 0, s);
+      break;
+    default:
+      launch_tile<DT_F32, 8, MODE_SCORES>(ix, n_splits, qblocks, 1, n_row_tiles, n, B, 1, 0, nullptr, out, ld, 0, s);
+      break;
+  }
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
 }
 
 int ahr_topk_merge(const uint64_t* keys_in, int B, int n_lists, int k_in, int k, float* scores,

@@ -5,6 +5,8 @@
 //                         (reference src/ah_rag/graph/hierarchical_graph.py:719-782):
 //                         seeds -> 1-hop expansion (belongs_to parents / members) -> rerank ->
 //                         stable sort on the 4-decimal rounded score -> top_k.
+//   lca_kernel            GraphEnvironment.expand_to_lca (environment.py:243-299): ancestor sets
+//                         on the belongs_to DAG by level-synchronous reverse BFS, intersected.
 //   expand_kernel         GraphEnvironment.expand_{parents,children,related}
 //                         (reference src/ah_rag/agent/environment.py:393-480), incl. the 2-hop
 //                         entity -> hyperedge -> co-participant walk of expand_related.
@@ -213,6 +215,121 @@ __global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
   out_count[q] = em.n;
 }
 
+// expand_to_lca (environment.py:243-299): per query, the intersection over its input nodes of
+// "ancestors or self" on the belongs_to DAG (nx.ancestors: nodes with a belongs_to path TO the
+// node, i.e. the reverse walk over belongs_to IN-edges), then its lowest members (no belongs_to
+// out-edge to another member). One 256-thread workgroup per query runs a level-synchronous
+// reverse BFS per input over the device CSR. Visited nodes live in an LDS hash table (open
+// addressing) whose slot holds (node, last input that reached it, number of inputs that reached
+// it): a discovery claims (node, input) with one atomic exchange on `last`, so each node enters
+// an input's frontier once and is counted once per input; a node is in the intersection iff its
+// count is the number of (non-padding) inputs. Capacities: kLcaHash distinct nodes per query, kLcaFront nodes per BFS level; a
+// query beyond them reports count -1 (the caller raises) instead of a wrong answer.
+constexpr int kLcaHash = 4096;  // power of two
+constexpr int kLcaFront = 1024;
+
+__device__ __forceinline__ uint32_t lca_hash(int32_t v) { return ((uint32_t)v * 2654435761u) & (kLcaHash - 1); }
+
+__global__ __launch_bounds__(256) void lca_kernel(DevGraph g, const int32_t* __restrict__ inputs, int n_in,
+                                                  int max_out, int32_t* __restrict__ out,
+                                                  int32_t* __restrict__ out_count) {
+  __shared__ int32_t hkey[kLcaHash];   // node id, -1 = empty
+  __shared__ int32_t hlast[kLcaHash];  // last input index that reached the node
+  __shared__ int32_t hcnt[kLcaHash];   // inputs that reached it
+  __shared__ int32_t front[2][kLcaFront];
+  __shared__ int32_t nfront[2];
+  __shared__ int32_t nout;
+  __shared__ int32_t overflow;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kLcaHash; i += 256) {
+    hkey[i] = -1;
+    hlast[i] = -1;
+    hcnt[i] = 0;
+  }
+  if (tid == 0) {
+    nout = 0;
+    overflow = 0;
+  }
+  // claim (v, input i): true the first time input i reaches v (v's slot is created if absent)
+  auto claim = [&](int32_t v, int i) -> bool {
+    uint32_t h = lca_hash(v);
+    for (int probe = 0; probe < kLcaHash; ++probe, h = (h + 1) & (kLcaHash - 1)) {
+      const int32_t prev = atomicCAS(&hkey[h], -1, v);
+      if (prev == -1 || prev == v) {
+        const int32_t last = atomicExch(&hlast[h], i);
+        if (last == i) return false;
+        atomicAdd(&hcnt[h], 1);
+        return true;
+      }
+    }
+    atomicOr(&overflow, 1);
+    return false;
+  };
+  auto lookup_count = [&](int32_t v) -> int32_t {
+    uint32_t h = lca_hash(v);
+    for (int probe = 0; probe < kLcaHash; ++probe, h = (h + 1) & (kLcaHash - 1)) {
+      if (hkey[h] == -1) return 0;
+      if (hkey[h] == v) return hcnt[h];
+    }
+    return 0;
+  };
+  __syncthreads();
+  int n_valid = 0;  // -1 entries pad a query's input list
+  for (int i = 0; i < n_in; ++i) {
+    const int32_t src = inputs[(int64_t)q * n_in + i];
+    if (src < 0 || src >= g.n_nodes) continue;  // uniform: every thread reads the same input
+    ++n_valid;
+    if (tid == 0) {
+      nfront[0] = 0;
+      nfront[1] = 0;
+      if (claim(src, i)) {
+        front[0][0] = src;
+        nfront[0] = 1;
+      }
+    }
+    __syncthreads();
+    int cur = 0;
+    while (nfront[cur] > 0) {
+      const int n = min(nfront[cur], kLcaFront);
+      for (int j = tid; j < n; j += 256) {
+        const int32_t v = front[cur][j];
+        for (int64_t e = g.off[ADJ_BT_IN][v]; e < g.off[ADJ_BT_IN][v + 1]; ++e) {
+          const int32_t u = g.tgt[ADJ_BT_IN][e];
+          if (!claim(u, i)) continue;
+          const int slot = atomicAdd(&nfront[cur ^ 1], 1);
+          if (slot < kLcaFront)
+            front[cur ^ 1][slot] = u;
+          else
+            atomicOr(&overflow, 1);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) nfront[cur] = 0;
+      __syncthreads();
+      cur ^= 1;
+    }
+    __syncthreads();
+  }
+  // lowest members of the intersection: no belongs_to out-edge to another member
+  for (int h = tid; h < kLcaHash; h += 256) {
+    const int32_t v = hkey[h];
+    if (v < 0 || n_valid == 0 || hcnt[h] != n_valid) continue;
+    bool lowest = true;
+    for (int64_t e = g.off[ADJ_BT_OUT][v]; e < g.off[ADJ_BT_OUT][v + 1] && lowest; ++e)
+      if (lookup_count(g.tgt[ADJ_BT_OUT][e]) == n_valid) lowest = false;
+    if (lowest) {
+      const int slot = atomicAdd(&nout, 1);
+      if (slot < max_out)
+        out[(int64_t)q * max_out + slot] = v;
+      else
+        atomicOr(&overflow, 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) out_count[q] = overflow ? -1 : min(nout, max_out);
+}
+
 }  // namespace graph
 }  // namespace ahr
 
@@ -326,6 +443,19 @@ int ahr_graph_destroy(ahr_graph* g) {
   DeviceGuardG dg(g->device);
   if (g->block) (void)hipFree(g->block);
   delete g;
+  return AHR_OK;
+}
+
+int ahr_graph_lca(ahr_graph* g, const int32_t* inputs, int B, int n_in, int max_out, int32_t* out,
+                  int32_t* out_count, void* stream) {
+  if (!g) return fail(AHR_EINVAL, "null graph");
+  if (B < 0 || n_in < 0 || max_out < 0) return fail(AHR_EINVAL, "negative size");
+  if (B == 0) return AHR_OK;
+  if ((n_in > 0 && !inputs) || !out_count || (max_out > 0 && !out)) return fail(AHR_EINVAL, "null buffer");
+  DeviceGuardG dg(g->device);
+  hipLaunchKernelGGL(lca_kernel, dim3((unsigned)B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), g->dg,
+                     inputs, n_in, max_out, out, out_count);
+  AHR_HIP(hipGetLastError());
   return AHR_OK;
 }
 

@@ -142,6 +142,13 @@ int ahr_index_query(ahr_index* ix, const float* q, int B, int k, int normalize_q
 int ahr_index_query_keys(ahr_index* ix, const float* q, int B, int k, int normalize_q,
                          int64_t row_base, uint64_t* keys, void* stream);
 
+/* Every score: out[b][r] = <q_b, row r> for the live rows r < count (device fp32, row pitch ld >=
+ * count), the fused tile kernel's GEMM core in scores mode (fp32 index: each score the k-ordered
+ * fma chain). Replaces the all-pairs np.dot loop of the L1 relation builder
+ * (src/ah_rag/aggregate/semantic_aggregator.py:620-661) with one device pass. */
+int ahr_index_scores(ahr_index* ix, const float* q, int B, int normalize_q, float* out, int64_t ld,
+                     void* stream);
+
 /* Merge n_lists descending key lists per query: keys_in device [B][n_lists][k_in] ->
  * top k as scores/rows (and optionally keys_out [B][k]). Used for the cross-shard merge
  * after the RCCL all-gather. */
@@ -213,6 +220,17 @@ int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float
  * node's neighbours were appended), first-occurrence dedupe and truncation to limit. */
 int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int n_in,
                      int limit, int32_t* out, int32_t* out_count, void* stream);
+
+/* Batched GraphEnvironment.expand_to_lca (environment.py:243-299): per query the nodes of the
+ * intersection of the inputs' "ancestors or self" sets on the belongs_to DAG (nx.ancestors: nodes
+ * with a belongs_to path to the input) that have no belongs_to out-edge to another member.
+ * inputs: device int32 [B][n_in] node indices, -1 = padding (queries of fewer inputs; a query
+ *   with no input has an empty result);
+ * out: device int32 [B][max_out] (unordered), out_count [B] (-1: the query exceeded the kernel's
+ * per-query capacity of 4096 visited nodes / 1024 per BFS level, or max_out). The caller sorts
+ * by (level, id) and truncates (:289), and checks acyclicity once per graph version. */
+int ahr_graph_lca(ahr_graph* g, const int32_t* inputs, int B, int n_in, int max_out, int32_t* out,
+                  int32_t* out_count, void* stream);
 
 int ahr_graph_info(const ahr_graph* g, int64_t* n_nodes, int64_t* n_edges);
 

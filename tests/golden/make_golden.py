@@ -259,6 +259,32 @@ def main() -> None:
                                  "include_hyperedges": True, "result": res})
         dump("search_cases.json", {"dim": 384, "model": "all-MiniLM-L6-v2", "cases": search_cases})
 
+        # ---- incremental re-index after node edits (build_vector_index upsert_only, :602-673)
+        hg3 = HierarchicalGraph.load(gdir)
+        db3 = os.path.join(work, "vector_db_up")
+        hg3.build_vector_index(db_path=db3, layers={0, 1}, upsert_only=False, reset=True)
+        before = dict(hg3.G.graph["vector_index"]["indexed_meta"])
+        probe = queries[:6] + ["a freshly edited description of entity three", "Topic 2 renamed"]
+        pre = [hg3.search(q, top_k=8, return_cluster=True, db_path=db3) for q in probe[:2]]
+        edits = [[eids[3], "description", "a freshly edited description of entity three"],
+                 [eids[10], "description", "Entity number ten now appears in passage 99"],
+                 [sids[2], "title", "Topic 2 renamed"]]
+        for nid, key, val in edits:
+            hg3.G.nodes[nid][key] = val
+        new_eid = hg3.add_entity(name="Entity Brand New", description="added after the first index build",
+                                 entity_type="person")
+        hg3.add_belongs_to(new_eid, sids[2], prob=0.5)
+        hg3.build_vector_index(db_path=db3, layers={0, 1}, upsert_only=True)
+        after = dict(hg3.G.graph["vector_index"]["indexed_meta"])
+        post = [{"query": q, "result": hg3.search(q, top_k=8, return_cluster=True, db_path=db3)} for q in probe]
+        dump("upsert_cases.json", {"edits": edits, "new_entity": {"name": "Entity Brand New", "id": new_eid,
+                                                                  "summary": sids[2]},
+                                   "indexed_meta_before": before, "indexed_meta_after": after,
+                                   "changed": sorted(k for k in after if before.get(k) != after[k]),
+                                   "pre": [{"query": q, "result": r} for q, r in zip(probe[:2], pre)],
+                                   "post": post, "vector_index": {k: v for k, v in hg3.G.graph["vector_index"].items()
+                                                                  if k != "db_path"}})
+
         # ---- GraphEnvironment scripts
         env_cases = []
         for q in queries[:10]:

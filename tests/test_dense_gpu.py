@@ -624,3 +624,24 @@ def test_small_f32_bit_exact(cuda, n, d, B, k, norm):
     np.testing.assert_array_equal(s[:, :kk].astype(np.float32), es[:, :kk].astype(np.float32))
     if kk < k:
         assert (r[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
+
+
+@pytest.mark.parametrize("dtype,n,d,B", [("f32", 3000, 768, 3000), ("f32", 517, 100, 33), ("bf16", 2000, 384, 129),
+                                         ("f32", 1, 64, 1)])
+def test_index_scores_matrix(cuda, dtype, n, d, B):
+    """ahr_index_scores (the tile kernel's GEMM core in scores mode, used by the L1 relation
+    builder): fp32 = the oracle's k-ordered fma chain bit for bit; bf16 within 1e-4 of f64."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(77 + n + B)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    S = ix.scores(Q).cpu().numpy()
+    ix.close()
+    assert S.shape == (B, n)
+    if dtype == "f32":
+        np.testing.assert_array_equal(S, dr.scores_matrix(C, Q, mode="fma"))
+    else:
+        ref = dr.scores_matrix(dr.round_to_storage(C, dtype), dr.round_to_storage(Q, dtype), mode="f64")
+        assert np.abs(S - ref).max() < 1e-4

@@ -125,3 +125,45 @@ def test_naive_rag_matches_reference(workdir):
     naive = NaiveRAG(hg, EchoGen())
     for c in _load("naive_cases.json")["cases"]:
         assert _norm(naive.run(c["query"], top_k=c["top_k"])) == c["out"]
+
+
+def test_incremental_reindex_matches_reference(workdir):
+    """§8f row 2: build_vector_index(upsert_only=True) after editing 3 nodes and adding one writes
+    only those 4 rows into the HBM-resident index (no reload of the store), with the reference's
+    indexed_meta, and search() then returns the reference's results."""
+    from ah_rag.graph.hierarchical_graph import HierarchicalGraph
+    case = _load("upsert_cases.json")
+    hg = HierarchicalGraph.load("graph")
+    hg.build_vector_index(db_path="vector_db_up", layers={0, 1}, upsert_only=False, reset=True)
+    assert hg.G.graph["vector_index"]["indexed_meta"] == case["indexed_meta_before"]
+    for c in case["pre"]:  # first search makes the index resident (one full load)
+        assert isclose_dicts(_norm(hg.search(c["query"], top_k=8, return_cluster=True, db_path="vector_db_up")),
+                             c["result"])
+    res = hg.resident_index("vector_db_up")
+    index_obj, loads = res.index, res.full_loads
+    for nid, key, val in case["edits"]:
+        hg.G.nodes[nid][key] = val
+    ne = case["new_entity"]
+    assert hg.add_entity(name=ne["name"], description="added after the first index build",
+                         entity_type="person") == ne["id"]
+    hg.add_belongs_to(ne["id"], ne["summary"], prob=0.5)
+    hg.build_vector_index(db_path="vector_db_up", layers={0, 1}, upsert_only=True)
+    vi = hg.G.graph["vector_index"]
+    assert vi["indexed_meta"] == case["indexed_meta_after"]
+    assert vi["indexed_nodes"] == case["vector_index"]["indexed_nodes"]
+    for c in case["post"]:
+        got = hg.search(c["query"], top_k=8, return_cluster=True, db_path="vector_db_up")
+        assert isclose_dicts(_norm(got), c["result"]), c["query"]
+    res = hg.resident_index("vector_db_up")
+    assert res.index is index_obj and res.full_loads == loads  # no reload, no reallocation
+    assert res.rows_upserted == len(case["changed"]) == 4
+    # the persisted store holds the same rows (a fresh process reloads them)
+    hg2 = HierarchicalGraph.load("graph")
+    hg2.G.graph["vector_index"] = dict(vi)
+    for nid, key, val in case["edits"]:
+        hg2.G.nodes[nid][key] = val
+    hg2.add_entity(name=ne["name"], description="added after the first index build", entity_type="person")
+    hg2.add_belongs_to(ne["id"], ne["summary"], prob=0.5)
+    c = case["post"][0]
+    assert isclose_dicts(_norm(hg2.search(c["query"], top_k=8, return_cluster=True, db_path="vector_db_up")),
+                         c["result"])

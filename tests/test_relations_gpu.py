@@ -1,4 +1,5 @@
-"""L1 topic relations on the GPU (centroid cosine as one fp32 GEMM) vs the reference outputs.
+"""L1 topic relations on the GPU (centroid cosine by the fp32 tile kernel, ahr_index_scores) vs the
+reference outputs.
 
 Tolerance: the GPU fp32 dot products may differ from numpy's float32 np.dot in the last bits, so
 cosine/weight are compared within 1e-4 after the reference's 4-dp rounding, and a pair may only

@@ -8,8 +8,10 @@ the vector store (no encoder weights offline), then times
             rerank for all E queries) and `steps` batched steps of random valid actions;
   * single: the drop-in AHRAGGymEnv stepped one environment at a time (B = 1 per call), the
             reference's own loop shape (policy_ppo.py:145,163-214) on the device graph.
-Replicas per GPU: one process per GPU, environments partitioned; no collective.
-Prints one JSON line. Usage: python tools/bench_env.py [--envs 1024] [--steps 6]
+Replicas per GPU: --gpus N runs one process per GPU (spawned by this script, or
+under torch.distributed.run), the graph and corpus replicated, the --envs environments
+partitioned over the ranks; no collective on the data path (the job time is the slowest rank's).
+Prints one JSON line. Usage: python tools/bench_env.py [--gpus 8] [--envs 1024] [--steps 6]
 """
 import argparse
 import json
@@ -23,9 +25,11 @@ sys.path[:0] = [os.path.join(ROOT, "ah-rag_amd"), ROOT]
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 from ah_rag.agent.gym_env import AHRAGGymEnv  # noqa: E402
 from ah_rag.agent.vec_env import VecAHRAGGymEnv  # noqa: E402
+from ah_rag.distributed import launch  # noqa: E402
 from ah_rag.graph.hierarchical_graph import HierarchicalGraph, VectorStore  # noqa: E402
 from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph  # noqa: E402
 
@@ -46,31 +50,42 @@ def random_actions(rng, masks):
     return [int(rng.choice(np.flatnonzero(np.asarray(m)))) for m in masks]
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--envs", type=int, default=1024)
-    ap.add_argument("--steps", type=int, default=6)
-    ap.add_argument("--single", type=int, default=32, help="environments stepped one by one")
-    a = ap.parse_args()
-    dev = torch.device("cuda", 0)
-    rng = np.random.default_rng(20251003)
+def run(a) -> None:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        # replicas: no collective on the data path, only the timing reduction
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    envs = a.envs // world + (1 if rank < a.envs % world else 0)  # environments partitioned over ranks
+    rng = np.random.default_rng(20251003 + rank)
     t0 = time.perf_counter()
     corpus = SyntheticCorpus(HOTPOT_90K, dev)
     vectors = corpus.rows().cpu().numpy()
-    hg, ids = build_hotpot_graph(corpus, rng)
+    hg, ids = build_hotpot_graph(corpus, np.random.default_rng(20251003))  # the same graph on every rank
     tmp = tempfile.mkdtemp(prefix="ahr_env_")
     install_vectors(hg, ids, vectors, os.path.join(tmp, "vector_db"))
-    q, _ = corpus.queries(a.envs, corpus.rows())
+    q, _ = corpus.queries(envs, corpus.rows(), salt=rank)
     qv = q.cpu().numpy()
-    queries = [f"query {i}" for i in range(a.envs)]
+    queries = [f"query {rank}.{i}" for i in range(envs)]
     t_build = time.perf_counter() - t0
 
-    venv = VecAHRAGGymEnv(n_envs=a.envs, max_steps=a.steps + 1, graph=hg)
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    venv = VecAHRAGGymEnv(n_envs=envs, max_steps=a.steps + 1, graph=hg)
     # warm-up episode: device graph, index, expansion kernels, host caches
-    venv.reset(queries[:a.envs], query_vectors=qv)
+    venv.reset(queries, query_vectors=qv)
     for _ in range(a.steps):
         venv.step(random_actions(rng, [e.get_action_mask() for e in venv.envs]))
-    torch.cuda.synchronize()
+    barrier()
     t1 = time.perf_counter()
     venv.reset(queries, query_vectors=qv)
     t_reset = time.perf_counter() - t1
@@ -81,39 +96,60 @@ def main():
         ts = time.perf_counter()
         venv.step(acts)
         step_times.append(time.perf_counter() - ts)
-    vec_steps = a.envs * (1 + a.steps)
-    vec_time = t_reset + sum(step_times)
+    barrier()
+    vec_time = time.perf_counter() - t1
+    if world > 1:  # job time = the slowest rank
+        t = torch.tensor([vec_time], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        vec_time = float(t.item())
+    vec_steps = a.envs * (1 + a.steps)  # all ranks' environments
 
-    # single-environment loop (B = 1 per search / expansion), a subset of the same queries
-    n1 = min(a.single, a.envs)
-    env = AHRAGGymEnv(max_steps=a.steps + 1, graph=hg)
-    env.env.logging_enabled = False
-    # one search first so the device graph / index are warm
-    hg.search_batch(queries[:1], top_k=5, return_cluster=True, query_vectors=qv[:1])
-    ts = time.perf_counter()
-    for i in range(n1):
-        # reset with a precomputed vector: the same path VecAHRAGGymEnv uses, at B = 1
-        sub = VecAHRAGGymEnv.__new__(VecAHRAGGymEnv)
-        sub.hg, sub.envs = hg, [env]
-        sub.reset([queries[i]], query_vectors=qv[i:i + 1])
-        for _ in range(a.steps):
-            env.step(random_actions(rng, [env.get_action_mask()])[0])
-    single_time = time.perf_counter() - ts
-    step_only = a.envs * a.steps / sum(step_times)
-    single_steps = n1 * (1 + a.steps)
+    single = None
+    if rank == 0 and a.single > 0:
+        # single-environment loop (B = 1 per search / expansion), a subset of the same queries
+        n1 = min(a.single, envs)
+        env = AHRAGGymEnv(max_steps=a.steps + 1, graph=hg)
+        env.env.logging_enabled = False
+        hg.search_batch(queries[:1], top_k=5, return_cluster=True, query_vectors=qv[:1])
+        ts = time.perf_counter()
+        for i in range(n1):
+            # reset with a precomputed vector: the same path VecAHRAGGymEnv uses, at B = 1
+            sub = VecAHRAGGymEnv.__new__(VecAHRAGGymEnv)
+            sub.hg, sub.envs = hg, [env]
+            sub.reset([queries[i]], query_vectors=qv[i:i + 1])
+            for _ in range(a.steps):
+                env.step(random_actions(rng, [env.get_action_mask()])[0])
+        single = round(n1 * (1 + a.steps) / (time.perf_counter() - ts), 1)
+    if rank == 0:
+        out = {
+            "metric": f"env steps/sec (reset + steps, 2-hop expand + rerank), C5 on {world} MI355X",
+            "n_gpus": world, "envs": a.envs, "envs_per_gpu": envs, "steps_per_episode": a.steps,
+            "vec_env_steps_per_s": round(vec_steps / vec_time, 1),
+            "vec_step_only_per_s_rank0": round(envs * a.steps / sum(step_times), 1),
+            "vec_reset_ms_rank0": round(t_reset * 1e3, 2), "vec_step_ms_rank0": [round(t * 1e3, 2) for t in step_times],
+            "single_env_steps_per_s": single,
+            "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
+            "build_s": round(t_build, 1), "parallelism": f"replicas{world} (environments partitioned, no collective)",
+            "data": "synthetic HotpotQA-distractor-shaped graph (SURVEY §8d), seeded corpus vectors, random valid actions",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
-    out = {
-        "metric": "env steps/sec (reset + steps, 2-hop expand + rerank), C5 on 1 MI355X",
-        "envs": a.envs, "steps_per_episode": a.steps,
-        "vec_env_steps_per_s": round(vec_steps / vec_time, 1),
-        "vec_step_only_per_s": round(step_only, 1),
-        "vec_reset_ms": round(t_reset * 1e3, 2), "vec_step_ms": [round(t * 1e3, 2) for t in step_times],
-        "single_env_steps_per_s": round(single_steps / single_time, 1), "single_envs": n1,
-        "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
-        "build_s": round(t_build, 1),
-        "data": "synthetic HotpotQA-distractor-shaped graph (SURVEY §8d), seeded corpus vectors, random valid actions",
-    }
-    print(json.dumps(out), flush=True)
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=1024, help="environments of the whole job")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--single", type=int, default=32, help="environments stepped one by one (rank 0)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
+    a = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        launch(a.gpus, run, (a,))  # one process per GPU, spawned before any GPU call
+        return
+    run(a)
 
 
 if __name__ == "__main__":
