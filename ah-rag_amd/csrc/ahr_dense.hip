@@ -2895,7 +2895,7 @@ struct ahr_index {
   int64_t row_stride = 0;
   int64_t count = 0;
   uint8_t* rows = nullptr;
-  uint8_t* rows_kb = nullptr;  // half types: k-blocked copy of rows (kb256::offset), kept in step by upsert
+  uint8_t* rows_kb = nullptr;  // half types, once the kb256 plan ran: k-blocked copy of rows (kb256::offset)
   uint8_t* qbuf = nullptr;
   uint8_t* qbuf_kb = nullptr;
   int64_t q_cap = 0;  // rows in qbuf (multiple of kRowPad)
@@ -3001,7 +3001,7 @@ bool small_ok(const ahr_index* ix, int B, int k) {
 // The k-blocked 256x256 kernel: half types (the k-blocked corpus copy exists), k <= 16; opt-in
 // (kFlagKB256) until it is measured ahead of the plans below.
 bool kb256_ok(const ahr_index* ix, int B, int k) {
-  if (k > 16 || ix->dtype == AHR_F32 || !ix->rows_kb) return false;
+  if (k > 16 || ix->dtype == AHR_F32) return false;
   if (ix->debug_flags & kFlagNoKB256) return false;
   return (ix->debug_flags & kFlagKB256) != 0 && B > 0;
 }
@@ -3108,11 +3108,6 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
     if (hipMalloc(&ix->qbuf, q_need * ix->row_stride) != hipSuccess)
       return fail(AHR_ENOMEM, "query workspace allocation failed");
     AHR_HIP(hipMemsetAsync(ix->qbuf, 0, q_need * ix->row_stride, s));
-    if (ix->rows_kb) {
-      if (hipMalloc(&ix->qbuf_kb, q_need * ix->row_stride) != hipSuccess)
-        return fail(AHR_ENOMEM, "query workspace allocation failed");
-      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, q_need * ix->row_stride, s));
-    }
     ix->q_cap = q_need;
   }
   // Partial lists: B x n_splits x k, sized for the worst case split count at this capacity.
@@ -3497,7 +3492,22 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     if (st) return st;
   }
   if (p.kernel == KERNEL_KB256 && ix->count > 0) {
+    // the k-blocked copies exist only once the kb256 plan is used (opt-in): built here, on this
+    // stream, the first time; upserts keep the corpus copy in step afterwards
     const int n_kb = ix->d_pad * ix->elem / kb256::kKB;
+    if (!ix->rows_kb) {
+      if (hipMalloc(&ix->rows_kb, ix->cap_pad * ix->row_stride) != hipSuccess)
+        return fail(AHR_ENOMEM, "k-blocked corpus allocation failed");
+      AHR_HIP(hipMemsetAsync(ix->rows_kb, 0, ix->cap_pad * ix->row_stride, s));
+      const int64_t all = ix->count * n_kb * 4;
+      hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(all, 256)), dim3(256), 0, s, ix->rows,
+                         ix->row_stride, (int64_t)0, ix->count, n_kb, ix->rows_kb);
+    }
+    if (!ix->qbuf_kb) {
+      if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
+        return fail(AHR_ENOMEM, "query workspace allocation failed");
+      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
+    }
     const int64_t chunks = (int64_t)B * n_kb * 4;
     hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->qbuf,
                        ix->row_stride, (int64_t)0, (int64_t)B, n_kb, ix->qbuf_kb);
@@ -3550,18 +3560,9 @@ int ahr_index_create(int dim, int dtype, int64_t capacity, int device, ahr_index
     delete ix;
     return fail(AHR_ENOMEM, "corpus allocation failed");
   }
-  // half types keep a k-blocked copy for the kb256 kernel (same bytes; 288 GB of HBM affords it)
-  if (dtype != AHR_F32 && hipMalloc(&ix->rows_kb, ix->cap_pad * ix->row_stride) != hipSuccess) {
-    (void)hipFree(ix->rows);
-    delete ix;
-    return fail(AHR_ENOMEM, "corpus allocation failed");
-  }
   // zeroed before any stream (also non-blocking ones) writes rows into it
-  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess ||
-      (ix->rows_kb && hipMemset(ix->rows_kb, 0, ix->cap_pad * ix->row_stride) != hipSuccess) ||
-      hipDeviceSynchronize() != hipSuccess) {
+  if (hipMemset(ix->rows, 0, ix->cap_pad * ix->row_stride) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     (void)hipFree(ix->rows);
-    if (ix->rows_kb) (void)hipFree(ix->rows_kb);
     delete ix;
     return fail(AHR_EHIP, "corpus memset failed");
   }
