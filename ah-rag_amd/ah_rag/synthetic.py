@@ -81,13 +81,13 @@ class SyntheticCorpus:
         s = self.spec
         g = torch.Generator(device="cpu").manual_seed(s.seed + 7919 * (salt + 1))
         half = batch // 2
-        n_rows = s.n_rows
+        if rows is None:
+            rows = self.rows()
+        n_rows = rows.shape[0]  # == spec.n_rows unless the caller truncated the corpus
         src = torch.randint(0, n_rows, (half,), generator=g)
         t = torch.randint(0, s.n_centroids, (batch - half,), generator=g)
         eps = torch.randn(batch, s.dim, generator=g) / np.sqrt(s.dim)
         eps = eps.to(self.device)
-        if rows is None:
-            rows = self.rows()
         base = torch.cat([rows[src.to(rows.device)].to(self.device),
                           self.centroids[t.to(self.device)]])
         scale = torch.cat([torch.full((half, 1), 0.2), torch.full((batch - half, 1), s.noise)]).to(self.device)

@@ -2905,7 +2905,7 @@ struct ahr_index {
   int64_t sample_cap = 0;   // floats
   uint8_t* cand = nullptr;  // query-resident kernel: candidate groups (counts, row bases, scores)
   int64_t cand_cap = 0;     // bytes
-  int sample_rows = 8192;   // S; 0 disables the threshold pre-pass
+  int sample_rows = -1;     // S; 0 disables the threshold pre-pass, -1 = sample_rows_for(count)
   // The fields above (qbuf .. cand_cap) are the ACTIVE query workspace; the others are parked
   // here (ahr_index_set_workspace swaps them) so batches on different streams never share one.
   ahr_query_ws parked[kMaxWorkspaces];
@@ -2974,6 +2974,15 @@ constexpr int kResidentSlots128 = 256 * 2;
 // candidate buffer's fallback list lives in private memory, and folding the buffer into it to
 // raise the threshold made the normal case slower, 591 vs 531 us at 4096). Debug flag kFlagQkv
 // plans it at any size.
+// Rows scored by the threshold pre-pass. The seed admits ~k * N / S candidates per query, so a
+// larger corpus wants a larger sample: S = 16384 from 512k rows on (5M x 768: tile kernel 8.87 vs
+// 9.10 ms at S = 8192, the pre-pass 49 vs 30 us; 625k: kb256 1.03 vs 1.06 ms, 312k: a wash),
+// 8192 below (C2, 90k rows: 16384 measured +12 us end to end).
+inline int sample_rows_for(const ahr_index* ix) {
+  if (ix->sample_rows >= 0) return ix->sample_rows;
+  return ix->count >= (1 << 19) ? 16384 : 8192;
+}
+
 bool qkv_ok(const ahr_index* ix, int B, int k) {
   const int nkt = ix->d_pad * ix->elem / kRowBytes;
   if (k > 16 || ix->dtype == AHR_F32 || !(nkt == 6 || nkt == 12)) return false;
@@ -2981,7 +2990,8 @@ bool qkv_ok(const ahr_index* ix, int B, int k) {
   if (ix->debug_flags & kFlagQkv) return true;
   // B <= 8192: at least 4 splits, so a producer's share of the survivors (~10 x N / S per query
   // on random-order data) fits its candidate buffer
-  return B >= 2048 && B <= 8192 && ix->sample_rows > 0 && ix->count <= 32 * (int64_t)ix->sample_rows;
+  const int S = sample_rows_for(ix);
+  return B >= 2048 && B <= 8192 && S > 0 && ix->count <= 32 * (int64_t)S;
 }
 
 // The small-batch streaming kernel: B <= 16 (<= 64 under kFlagSmallWide), bf16/f16, k <= 16, the
@@ -2998,12 +3008,18 @@ bool small_ok(const ahr_index* ix, int B, int k) {
   return small::lds_bytes(ix->row_stride, 16, small::groups(B)) <= 160 * 1024;
 }
 
-// The k-blocked 256x256 kernel: half types (the k-blocked corpus copy exists), k <= 16; opt-in
-// (kFlagKB256) until it is measured ahead of the plans below.
+// The k-blocked 256x256 kernel (bf16/f16, k <= 16) from kKB256MinRows corpus rows on: there the
+// corpus streams from HBM and its 3-step-deep ring beats the 128x128 kernel's 1-step one (5M
+// rows, B = 1024: 8.11 vs 9.04 ms; 1.25M: 1.97 vs 2.31 ms; 625k: 1.03 vs 1.17 ms; 312k: equal;
+// at 90k, L2/MALL-resident, the 128x128 kernel is ahead, 152 vs 209 us). Debug flags force it
+// (kFlagKB256) or keep it out (kFlagNoKB256).
+constexpr int64_t kKB256MinRows = 1 << 19;
 bool kb256_ok(const ahr_index* ix, int B, int k) {
-  if (k > 16 || ix->dtype == AHR_F32) return false;
+  if (k > 16 || ix->dtype == AHR_F32 || B <= 0) return false;
   if (ix->debug_flags & kFlagNoKB256) return false;
-  return (ix->debug_flags & kFlagKB256) != 0 && B > 0;
+  if (ix->debug_flags & kFlagKB256) return true;
+  if (ix->debug_flags & kKernelFlags) return false;  // another kernel explicitly requested
+  return ix->count >= kKB256MinRows;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
@@ -3321,7 +3337,7 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       return;
     }
   }
-  const int S = ix->sample_rows;
+  const int S = sample_rows_for(ix);
   if (S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
     // Threshold pre-pass: score the first S rows, take each query's k-th best.
     float* scores = ix->sample;
@@ -3719,8 +3735,8 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum, int* n_calls) {
 
 int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
   if (!ix) return fail(AHR_EINVAL, "null index");
-  if (rows < 0 || rows > kSampleMax || (rows & (rows - 1)) || (rows && rows < 256))
-    return fail(AHR_EINVAL, "sample rows must be 0 or a power of two in [256, 16384]");
+  if (rows < -1 || rows > kSampleMax || (rows > 0 && ((rows & (rows - 1)) || rows < 256)))
+    return fail(AHR_EINVAL, "sample rows must be -1 (automatic), 0 or a power of two in [256, 16384]");
   ix->sample_rows = rows;
   return AHR_OK;
 }

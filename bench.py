@@ -50,7 +50,7 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f16": 2500.0, "f32": 157.3}  # MI355X_MICRO
 HBM_PEAK_GBS = 8000.0
 KERNEL_NAMES = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
                 "tilelane128": "topk_tilelane_kernel", "t256": "topk_t256_kernel",
-                "qkv128": "topk_qkv_kernel"}
+                "qkv128": "topk_qkv_kernel", "kb256": "topk_kb256_kernel"}
 
 
 def parse_args(argv=None):

@@ -100,14 +100,16 @@ int ahr_index_read(const ahr_index* ix, int64_t start, int64_t n, float* out, vo
 int ahr_index_profile_begin(ahr_index* ix, int max_calls);
 int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_calls);
 
-/* Rows scored by the threshold pre-pass (0 disables it; else a power of two in [128, 1024]). */
+/* Rows scored by the threshold pre-pass: -1 = automatic (default: 8192, 16384 from 512k rows on),
+ * 0 disables it, else a power of two in [256, 16384]. */
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
 /* Ablation switches for profiling, never set in production. Correct results: 8 = always the
  * 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile kernel at any
  * batch (k <= 16), 64 = the 256x128 lane kernel (k <= 16), 2048 = no query-resident kernel,
  * 4096 = the query-resident kernel wherever it applies, 32768 = the 256x256 16x16x32 kernel,
- * 65536 = the small-batch streaming kernel up to B = 64. Garbage results (cost splits):
+ * 65536 = the small-batch streaming kernel up to B = 64, 131072 = the k-blocked 256x256 kernel
+ * wherever it applies, 262144 = never the k-blocked kernel. Garbage results (cost splits):
  * 2 = skip the top-k epilogue, 256 = lane epilogue stops after the group maxima, 512 = tile
  * kernel (cooperative) loads operands for its first tile only. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
@@ -116,7 +118,8 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags);
  * *kernel: 0 = 128x128 tile kernel (cooperative screening; k > 16), 1 = 256x256 lane kernel
  * (k <= 16, B >= 6144), 2 = 256x128 lane kernel, 3 = 128x128 lane-local tile kernel (k <= 16,
  * B < 6144), 5 = query-resident kernel (bf16/f16, 2048 <= B <= 8192), 6 = 256x256 16x16x32
- * kernel (opt-in), 7 = small-batch streaming kernel (bf16/f16, B <= 16, k <= 16). */
+ * kernel (opt-in), 7 = small-batch streaming kernel (bf16/f16, B <= 16, k <= 16), 8 = k-blocked
+ * 256x256 kernel (bf16/f16, k <= 16, from 512k corpus rows). */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 

@@ -35,16 +35,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="hotpot90k")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--rows", type=int, default=0, help="use only the first ROWS corpus rows (0 = all)")
     ap.add_argument("--batches", default="1,64,256,1024,4096")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="prod:8192:0,tile128:8192:8,lane256x128:8192:64,no_prepass:0:0,gemm_only:0:2,max_only:8192:256")
+    ap.add_argument("--variants", default="prod:-1:0,tile128:-1:8,kb256:-1:131072,no_prepass:0:0,gemm_only:-1:2,max_only:-1:256")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     spec = HOTPOT_90K if a.workload == "hotpot90k" else SYNTH_5M
     c = SyntheticCorpus(spec, dev)
     rows = c.rows()
+    if a.rows:
+        rows = rows[:a.rows].contiguous()
     ix = DenseIndex(rows.shape[1], rows.shape[0], dtype=a.dtype, device=dev)
     for s in range(0, rows.shape[0], 1_000_000):
         ix.upsert(rows[s:s + 1_000_000], start=s)
@@ -59,7 +62,7 @@ def main():
                 ix.set_debug_flags(flags)
                 t = run(ix, q, a.k, a.steps)
                 res.setdefault(name, []).append(t)
-        ix.set_sample_rows(8192)
+        ix.set_sample_rows(-1)
         ix.set_debug_flags(0)
         best = {n: min(v, key=lambda d: sum(d.values())) for n, v in res.items()}
         flops = 2.0 * B * rows.shape[0] * rows.shape[1]

@@ -72,7 +72,7 @@ def main() -> None:
         if base not in ("topk_tile_kernel", "topk_tilelane_kernel", "topk_lane_kernel", "topk_qkv_kernel", "topk_t256_kernel",
                         "topk_small_kernel", "topk_small_f32_kernel", "merge_block_kernel", "merge_lane_lists_kernel", "merge_heads_kernel",
                         "merge_kernel", "sample_kth_kernel", "convert_rows_kernel", "expand_rerank_kernel",
-                        "expand_kernel"):
+                        "expand_kernel", "topk_kb256_kernel", "reblock_kb_kernel", "lca_kernel"):
             continue
         rec = out.setdefault(base, {"variants": {}})
         f = fetch.get(k, {}).get("FETCH_SIZE", [])
