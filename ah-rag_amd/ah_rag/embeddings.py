@@ -211,7 +211,7 @@ class DenseIndex:
         256x256 16x16x32 kernel (bf16/f16, k <= 16), 65536 = the small-batch kernel up to B = 64."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
-    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256")
+    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256", "kb128")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

@@ -192,10 +192,11 @@ enum {
   kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
   kFlagSmallWide = 65536,  // the small-batch kernel up to B = 64 (2 or 4 query groups; measured slower)
   kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagNoKB256 = 262144,  // plan without the k-blocked kernel
+  kFlagNoKB256 = 262144,  // plan without the k-blocked kernels
+  kFlagKB128 = 524288,    // the k-blocked 256x128 kernel wherever it applies (bf16/f16, k <= 16)
 };
-constexpr int kKernelFlags =
-    kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 | kFlagKB256 | kFlagNoKB256;
+constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
+                             kFlagKB256 | kFlagNoKB256 | kFlagKB128;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
@@ -1406,7 +1407,8 @@ __global__ __launch_bounds__(512, 1) void topk_t256_kernel(
 // topk_kb256_kernel (bf16/f16, k <= 16; the default from B = 17): the t256 tile (256 corpus rows x
 // 256 queries, 8 waves = 2 along rows x 4 along queries, a 128 x 64 block of 16x16x32 MFMAs per
 // wave, 128 accumulator VGPRs, one workgroup per CU) fed from a K-BLOCKED copy of the corpus and
-// of the queries: [tile of 256 rows][32-deep k-block][256 rows][64 B]. A 32-deep k-step of a tile
+// of the queries: [tile of 256 rows][32-deep k-block][256 rows][64 B].
+// A 32-deep k-step of a tile
 // is then one contiguous 16-KiB block whose 128-B lines are whole (row pairs), so the k-steps can
 // be 32 deep without splitting lines between two requests (the cost that sank 64-B half rows in
 // the row-major kernels), and 32-KiB stages leave room for a 4-stage ring: each k-step issues the
@@ -1425,9 +1427,11 @@ constexpr int kStage = 2 * kBlock;               // A (corpus) block, then B (qu
 constexpr int kStages = 4;
 constexpr int kLds = kStages * kStage;           // 128 KiB
 static_assert(kLds <= 160 * 1024, "kb256 LDS exceeds 160 KiB");
+// block index of k-block kb of tile t
+__host__ __device__ __forceinline__ int64_t block(int64_t t, int kb, int n_kb) { return t * n_kb + kb; }
 // byte offset of (row, k-block) in a k-blocked buffer of n_kb k-blocks
 __host__ __device__ __forceinline__ int64_t offset(int64_t row, int kb, int n_kb) {
-  return (((row >> 8) * n_kb + kb) * kTR + (row & 255)) * kKB;
+  return (block(row >> 8, kb, n_kb) * kTR + (row & 255)) * kKB;
 }
 // LDS image of a 64-B row: logical 16-B chunk c of row r sits in physical slot c ^ h(r), h(r) =
 // (-(r >> 2)) & 3. A 256-B bank row holds 4 rows; a ds_read_b128 lane group of the 16x16x32
@@ -1451,19 +1455,46 @@ __global__ __launch_bounds__(256) void reblock_kb_kernel(const uint8_t* __restri
   *reinterpret_cast<u32x4*>(dst + kb256::offset(row, ch >> 2, n_kb) + (ch & 3) * 16) = v;
 }
 
-template <int DT, int KCAP>
-__global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
+// The same kernel with WN = 2 waves along queries ("kb128": 256 rows x 128 queries, 4 waves, two
+// workgroups per CU, a 3-stage ring of 24-KiB steps, 72 KiB of LDS): the wave tile, fragment map,
+// k order and epilogue are unchanged, so scores and rows are bitwise kb256's; two independent
+// workgroups per CU cover each other's barriers, fragment-read latency and epilogue, which eight
+// waves in lock-step (one workgroup per CU) do not.
+template <int WN>
+struct KbCfg {
+  static constexpr int kWaves = 2 * WN;
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kTQ = 64 * WN;                        // queries per workgroup
+  static constexpr int kBBlock = kTQ * kb256::kKB;           // one k-step of the query block
+  static constexpr int kStageBytes = kb256::kBlock + kBBlock;
+  static constexpr int kStages = WN == 4 ? 4 : 3;
+  static constexpr int kLds = kStages * kStageBytes;
+  static constexpr int kAPieces = 16 / kWaves;               // 1-KiB DMA pieces per wave and k-step
+  static constexpr int kBPieces = kTQ / 16 / kWaves;
+  static constexpr int kPieces = kAPieces + kBPieces;
+  static constexpr int kMinBlocks = WN == 4 ? 1 : 2;
+  static_assert(kLds * kMinBlocks <= 160 * 1024, "k-blocked kernel LDS exceeds 160 KiB per CU");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int DT, int KCAP, int WN>
+__global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void topk_kb256_kernel(
     const uint8_t* __restrict__ corpus_kb, const uint8_t* __restrict__ queries_kb, int n_kb, int n_rows, int n_q,
     int n_row_tiles, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
     const float* __restrict__ thr_init, int n_splits, int qblocks, int flags, uint64_t* __restrict__ cand_keys,
     int cand_cap) {
   static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
+  using C = KbCfg<WN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 2;  // 128-row half of the tile
-  const int wn = wave & 3;   // 64-query quarter of the block
+  const int wm = wave / WN;  // 128-row half of the tile
+  const int wn = wave % WN;  // 64-query block of the workgroup's queries
   const int fr = lane & 15;
   const int fq = lane >> 4;
   int split, qb;
@@ -1476,7 +1507,7 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
     split = blockIdx.x % n_splits;
     qb = blockIdx.x / n_splits;
   }
-  const int q0 = qb * kb256::kTQ;
+  const int q0 = qb * C::kTQ;
   const int t_begin = (int)((int64_t)split * n_row_tiles / n_splits);
   const int t_end = (int)((int64_t)(split + 1) * n_row_tiles / n_splits);
 
@@ -1504,28 +1535,32 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
   const int total = (t_end - t_begin) * n_kb;  // k-steps of this workgroup
   if (total > 0) {
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    // DMA: per 16-KiB block, wave w fills rows [16w, 16w + 16) (j = 0) and [128 + 16w, ...) (j = 1),
+    // DMA: per block, wave w fills the 16-row pieces w, w + waves, w + 2 waves, ... (1 KiB each),
     // lane l at (row 16w + l/4, physical slot l%4), loading the logical chunk whose kb256::phys is
-    // l%4 (phys is an involution in the chunk): every ds_read_b128 lane group hits 16 distinct
-    // 16-B bank slots
+    // l%4 (phys is an involution in the chunk, and rows 16 apart share it): every ds_read_b128
+    // lane group hits 16 distinct 16-B bank slots
+    constexpr int kPieceStride = C::kWaves * 16 * kb256::kKB;
     const int lrow = wave_u * 16 + (lane >> 2);
     const uint32_t voff = (uint32_t)(lrow * kb256::kKB + (kb256::phys(lane & 3, lrow) << 4));
-    const uint8_t* qblk = queries_kb + (int64_t)qb * n_kb * kb256::kBlock;
-    auto issue = [&](int c) __attribute__((always_inline)) {
+    // the workgroup's queries: rows (q0 & 255) .. + kTQ of each k-block of their 256-query tile
+    const uint8_t* qblk = queries_kb + (q0 & 255) * kb256::kKB;
+    auto issue = [&](int c, int stage) __attribute__((always_inline)) {
       const int t = t_begin + c / n_kb;
       const int kb = c % n_kb;
       const __amdgpu_buffer_rsrc_t a_rsrc =
-          tile_rsrc(corpus_kb + ((int64_t)t * n_kb + kb) * kb256::kBlock, kb256::kBlock);
-      const __amdgpu_buffer_rsrc_t b_rsrc = tile_rsrc(qblk + (int64_t)kb * kb256::kBlock, kb256::kBlock);
-      unsigned char* dst = smem + (c & (kb256::kStages - 1)) * kb256::kStage + wave_u * 16 * kb256::kKB;
+          tile_rsrc(corpus_kb + kb256::block(t, kb, n_kb) * kb256::kBlock, kb256::kBlock);
+      const __amdgpu_buffer_rsrc_t b_rsrc =
+          tile_rsrc(qblk + kb256::block(q0 >> 8, kb, n_kb) * kb256::kBlock, C::kBBlock);
+      unsigned char* dst = smem + stage * C::kStageBytes + wave_u * 16 * kb256::kKB;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (__attribute__((address_space(3))) void*)(dst + j * 8192),
-                                                 16, voff, j * 8192, 0, 0);
+      for (int j = 0; j < C::kAPieces; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            b_rsrc, (__attribute__((address_space(3))) void*)(dst + kb256::kBlock + j * 8192), 16, voff, j * 8192, 0,
-            0);
-      }
+            a_rsrc, (__attribute__((address_space(3))) void*)(dst + j * kPieceStride), 16, voff, j * kPieceStride, 0, 0);
+#pragma unroll
+      for (int j = 0; j < C::kBPieces; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            b_rsrc, (__attribute__((address_space(3))) void*)(dst + kb256::kBlock + j * kPieceStride), 16, voff,
+            j * kPieceStride, 0, 0);
     };
     // fragment reads: lane l reads row l & 15, logical chunk l / 16 (k 8(l/16) .. +8 of the step)
     const uint32_t fo = (uint32_t)(fr * kb256::kKB + (kb256::phys(fq, fr) << 4));
@@ -1544,40 +1579,59 @@ __global__ __launch_bounds__(512, 1) void topk_kb256_kernel(
       if (kth) thr[nb] = fmaxf(thr[nb], key_score(kth));
     };
 
-    const int pro = total < 3 ? total : 3;
-    for (int c = 0; c < pro; ++c) issue(c);
+    constexpr int kAhead = C::kStages - 1;  // k-steps in flight ahead of the one being multiplied
+    const int pro = total < kAhead ? total : kAhead;
+    for (int c = 0; c < pro; ++c) issue(c, c);
     int t = t_begin;
     int kb = 0;
+    int st_c = 0;                 // stage of step c
+    int st_i = kAhead % C::kStages;  // stage of step c + kAhead (= step c - 1's)
     for (int c = 0; c < total; ++c) {
-      // this wave's DMA of step c landed: leave the steps issued after it (up to 2) in flight
+      // this wave's DMA of step c landed: leave the steps issued after it (up to kAhead - 1) in flight
       const int ahead = total - 1 - c;
       if (!(flags & kFlagNoWait)) {
-        if (ahead >= 2)
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (ahead == 1)
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (kAhead == 3) {
+          if (ahead >= 2)
+            wait_vmcnt<2 * C::kPieces>();
+          else if (ahead == 1)
+            wait_vmcnt<C::kPieces>();
+          else
+            wait_vmcnt<0>();
+        } else {
+          if (ahead >= 1)
+            wait_vmcnt<C::kPieces>();
+          else
+            wait_vmcnt<0>();
+        }
       }
       lds_barrier();  // everyone's step c landed; everyone finished reading step c - 1
-      if (c + 3 < total && !((flags & kFlagNoLoads) && c >= 1)) issue(c + 3);  // into step c - 1's stage
-      if (kb == 0) {
-#pragma unroll
-        for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      const unsigned char* st = smem + (c & (kb256::kStages - 1)) * kb256::kStage;
+      if (c + kAhead < total && !((flags & kFlagNoLoads) && c >= 1)) issue(c + kAhead, st_i);  // into step c - 1's stage
+      const unsigned char* st = smem + st_c * C::kStageBytes;
+      st_c = st_c + 1 == C::kStages ? 0 : st_c + 1;
+      st_i = st_i + 1 == C::kStages ? 0 : st_i + 1;
       const unsigned char* abase = st + (wm * 128) * kb256::kKB + fo;
       const unsigned char* bbase = st + kb256::kBlock + (wn * 64) * kb256::kKB + fo;
       u32x4 b[4];
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) b[nb] = *reinterpret_cast<const u32x4*>(bbase + nb * 16 * kb256::kKB);
+      if (kb == 0) {  // a tile's first k-step accumulates onto an inline-constant 0 (no register zeroing)
 #pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-        const u32x4 a = *reinterpret_cast<const u32x4*>(abase + mb * 16 * kb256::kKB);
+        for (int mb = 0; mb < 8; ++mb) {
+          const u32x4 a = *reinterpret_cast<const u32x4*>(abase + mb * 16 * kb256::kKB);
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb) mfma16(a, b[nb], acc[mb][nb], DT);
+          for (int nb = 0; nb < 4; ++nb) {
+            f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            mfma16(a, b[nb], z, DT);
+            acc[mb][nb] = z;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb) {
+          const u32x4 a = *reinterpret_cast<const u32x4*>(abase + mb * 16 * kb256::kKB);
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) mfma16(a, b[nb], acc[mb][nb], DT);
+        }
       }
       if (++kb < n_kb) continue;
       kb = 0;
@@ -2948,7 +3002,7 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 // 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed), 6 = 256x256 16x16x32
 // kernel (opt-in), 7 = small-batch streaming kernel (B <= 16; <= 64 opt-in)
 enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
-       KERNEL_T256 = 6, KERNEL_SMALL = 7, KERNEL_KB256 = 8 };
+       KERNEL_T256 = 6, KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_KB128 = 9 };
 
 struct SearchPlan {
   int kernel;
@@ -2986,7 +3040,7 @@ inline int sample_rows_for(const ahr_index* ix) {
 bool qkv_ok(const ahr_index* ix, int B, int k) {
   const int nkt = ix->d_pad * ix->elem / kRowBytes;
   if (k > 16 || ix->dtype == AHR_F32 || !(nkt == 6 || nkt == 12)) return false;
-  if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres)) return false;
+  if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagKB128)) return false;
   if (ix->debug_flags & kFlagQkv) return true;
   // B <= 8192: at least 4 splits, so a producer's share of the survivors (~10 x N / S per query
   // on random-order data) fits its candidate buffer
@@ -3016,10 +3070,15 @@ bool small_ok(const ahr_index* ix, int B, int k) {
 constexpr int64_t kKB256MinRows = 1 << 19;
 bool kb256_ok(const ahr_index* ix, int B, int k) {
   if (k > 16 || ix->dtype == AHR_F32 || B <= 0) return false;
-  if (ix->debug_flags & kFlagNoKB256) return false;
+  if (ix->debug_flags & (kFlagNoKB256 | kFlagKB128)) return false;
   if (ix->debug_flags & kFlagKB256) return true;
   if (ix->debug_flags & kKernelFlags) return false;  // another kernel explicitly requested
   return ix->count >= kKB256MinRows;
+}
+
+bool kb128_ok(const ahr_index* ix, int B, int k) {
+  if (k > 16 || ix->dtype == AHR_F32 || B <= 0) return false;
+  return (ix->debug_flags & kFlagKB128) != 0;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
@@ -3049,12 +3108,13 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     return p;
   }
-  if (kb256_ok(ix, B, k)) {
-    // 256x256 tiles, one workgroup per CU: one wave of 256 workgroups
-    p.kernel = KERNEL_KB256;
-    p.qblocks = (int)cdiv(B, kb256::kTQ);
+  if (kb128_ok(ix, B, k) || kb256_ok(ix, B, k)) {
+    // 256x256 tiles, one workgroup per CU, or 256x128 tiles, two per CU: one wave of workgroups
+    const bool w128 = kb128_ok(ix, B, k);
+    p.kernel = w128 ? KERNEL_KB128 : KERNEL_KB256;
+    p.qblocks = (int)cdiv(B, w128 ? KbCfg<2>::kTQ : KbCfg<4>::kTQ);
     p.n_row_tiles = (int)cdiv(ix->count, kb256::kTR);
-    int want = std::max(1, 256 / p.qblocks);
+    int want = std::max(1, (w128 ? 512 : 256) / p.qblocks);
     want = std::min(want, std::max(1, p.n_row_tiles));
     p.xcd_remap = want >= 8;
     p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
@@ -3130,7 +3190,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
   const int64_t qblocks = cdiv(B, kTileQ);
   const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlots128, qblocks)), 8) * 8;
   const int64_t wide_splits = std::max<int64_t>(1, 512 / cdiv(B, 128));  // >= any plan's
-  const int64_t t256_lists = 2 * std::max<int64_t>(1, 256 / cdiv(B, 256));  // (split, row half) lists
+  const int64_t t256_lists = 2 * std::max<int64_t>(1, 512 / cdiv(B, 128));  // (split, row half) lists: kb128 >= kb256
   const int64_t p_need = (int64_t)B *
                          std::max<int64_t>(std::max(std::max(max_splits, wide_splits), t256_lists), kSampleMax / kTileRows) *
                          k;
@@ -3199,7 +3259,7 @@ void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B
 // lane's private list inside the kernel, so the cap only trades memory for speed.
 inline int qkv_cand_cap(const SearchPlan& p) { return (int)std::min(64, std::max(16, p.tiles_per_split)); }
 inline int64_t cand_bytes(int B, const SearchPlan& p) {
-  const int64_t prod = (p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) ? 8 : 4;  // producers per (query, split)
+  const int64_t prod = (p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256 || p.kernel == KERNEL_KB128) ? 8 : 4;  // producers per (query, split)
   return (int64_t)B * prod * p.n_splits * qkv_cand_cap(p) * 8;
 }
 
@@ -3236,13 +3296,14 @@ void launch_t256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
                      thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
 
-template <int DT, int KCAP>
+template <int DT, int KCAP, int WN>
 void launch_kb256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                   const float* thr, int flags, hipStream_t s) {
-  constexpr auto kern = &topk_kb256_kernel<DT, KCAP>;
+  using C = KbCfg<WN>;
+  constexpr auto kern = &topk_kb256_kernel<DT, KCAP, WN>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), kb256::kLds);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(512), kb256::kLds, s, ix->rows_kb,
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), C::kLds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(C::kThreads), C::kLds, s, ix->rows_kb,
                      ix->qbuf_kb, ix->d_pad * ix->elem / kb256::kKB, n_rows, B, p.n_row_tiles, row_base, k, ix->part,
                      thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
@@ -3354,11 +3415,20 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   if constexpr (DT != DT_F32) {
     if (p.kernel == KERNEL_KB256) {
       if (k <= 8)
-        launch_kb256<DT, 8>(ix, p, n, B, k, row_base, thr, flags, s);
+        launch_kb256<DT, 8, 4>(ix, p, n, B, k, row_base, thr, flags, s);
       else if (k <= 12)
-        launch_kb256<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s);
+        launch_kb256<DT, 12, 4>(ix, p, n, B, k, row_base, thr, flags, s);
       else
-        launch_kb256<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s);
+        launch_kb256<DT, 16, 4>(ix, p, n, B, k, row_base, thr, flags, s);
+      return;
+    }
+    if (p.kernel == KERNEL_KB128) {
+      if (k <= 8)
+        launch_kb256<DT, 8, 2>(ix, p, n, B, k, row_base, thr, flags, s);
+      else if (k <= 12)
+        launch_kb256<DT, 12, 2>(ix, p, n, B, k, row_base, thr, flags, s);
+      else
+        launch_kb256<DT, 16, 2>(ix, p, n, B, k, row_base, thr, flags, s);
       return;
     }
     if (p.kernel == KERNEL_T256) {
@@ -3503,11 +3573,13 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     }
   }
   SearchPlan p = plan_search(ix, B, k);
-  if ((p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) && ix->count > 0) {
+  const bool kb_plan = p.kernel == KERNEL_KB256 || p.kernel == KERNEL_KB128;
+  const bool cand_plan = p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || kb_plan;
+  if (cand_plan && ix->count > 0) {
     st = ensure_cand(ix, cand_bytes(B, p));
     if (st) return st;
   }
-  if (p.kernel == KERNEL_KB256 && ix->count > 0) {
+  if (kb_plan && ix->count > 0) {
     // the k-blocked copies exist only once the kb256 plan is used (opt-in): built here, on this
     // stream, the first time; upserts keep the corpus copy in step afterwards
     const int n_kb = ix->d_pad * ix->elem / kb256::kKB;
@@ -3541,7 +3613,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   prof_mark(ix, 3, s);
   {
     // qkv: one list per (split, dimension half); t256 / kb256: one per (split, row half)
-    const int lists = (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256 ? 2 : 1) *
+    const int lists = (cand_plan ? 2 : 1) *
                       p.n_splits;
     launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
   }
@@ -3797,7 +3869,7 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
   // candidate groups of the query-resident plan at the current corpus size
   for (int kk = 1; kk <= max_k; kk = kk < 8 ? 8 : kk + 8) {
     const SearchPlan p = plan_search(ix, max_batch, kk);
-    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) {
+    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256 || p.kernel == KERNEL_KB128) {
       st = ensure_cand(ix, cand_bytes(max_batch, p));
       if (st) return st;
     }

@@ -109,7 +109,8 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows);
  * batch (k <= 16), 64 = the 256x128 lane kernel (k <= 16), 2048 = no query-resident kernel,
  * 4096 = the query-resident kernel wherever it applies, 32768 = the 256x256 16x16x32 kernel,
  * 65536 = the small-batch streaming kernel up to B = 64, 131072 = the k-blocked 256x256 kernel
- * wherever it applies, 262144 = never the k-blocked kernel. Garbage results (cost splits):
+ * wherever it applies, 262144 = never the k-blocked kernels, 524288 = the k-blocked 256x128 kernel
+ * (two workgroups per CU) wherever it applies. Garbage results (cost splits):
  * 2 = skip the top-k epilogue, 256 = lane epilogue stops after the group maxima, 512 = tile
  * kernel (cooperative) loads operands for its first tile only. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
@@ -119,7 +120,7 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags);
  * (k <= 16, B >= 6144), 2 = 256x128 lane kernel, 3 = 128x128 lane-local tile kernel (k <= 16,
  * B < 6144), 5 = query-resident kernel (bf16/f16, 2048 <= B <= 8192), 6 = 256x256 16x16x32
  * kernel (opt-in), 7 = small-batch streaming kernel (bf16/f16, B <= 16, k <= 16), 8 = k-blocked
- * 256x256 kernel (bf16/f16, k <= 16, from 512k corpus rows). */
+ * 256x256 kernel (bf16/f16, k <= 16, from 512k corpus rows), 9 = k-blocked 256x128 kernel (opt-in). */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 

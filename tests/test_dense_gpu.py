@@ -472,7 +472,34 @@ def test_kb256_matches_t256(cuda, dtype, n, d, B, k, sample):
     assert np.abs(a[0][:, :kk] - es[:, :kk]).max() < 1e-4
 
 
-def test_kb256_slot_upsert_and_ties(cuda):
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n,d,B,k,sample", [
+    (40001, 768, 1024, 10, 8192), (33000, 384, 300, 16, 8192), (300, 768, 1, 1, 0), (1000, 128, 257, 8, 0),
+    (5000, 100, 17, 12, 0), (4000, 1100, 40, 10, 0), (90000, 768, 1024, 10, 8192), (90000, 768, 200, 10, 8192)])
+def test_kb128_matches_kb256(cuda, dtype, n, d, B, k, sample):
+    """kb128 (256 rows x 128 queries, two workgroups per CU, 3-stage ring) keeps kb256's wave tile,
+    fragment map and k order: scores and rows bitwise equal; odd query blocks (the upper half of a
+    256-query k-block), ragged tiles, splits without tiles, no seed."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(291 + n + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    ix.set_sample_rows(sample)
+    ix.set_debug_flags(524288)
+    assert ix.plan(B, k)["kernel"] == "kb128"
+    a = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(131072)
+    assert ix.plan(B, k)["kernel"] == "kb256"
+    b = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.close()
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0], b[0])
+
+
+@pytest.mark.parametrize("flag,name", [(131072, "kb256"), (524288, "kb128")])
+def test_kb256_slot_upsert_and_ties(cuda, flag, name):
     """Scattered-slot upserts refresh the k-blocked copy; duplicate rows order by row id."""
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(23)
@@ -482,9 +509,9 @@ def test_kb256_slot_upsert_and_ties(cuda):
     ix.upsert(np.zeros_like(C))
     perm = rng.permutation(len(C))
     ix.upsert(C[perm], slots=perm)
-    ix.set_debug_flags(131072)
+    ix.set_debug_flags(flag)
     pick = rng.integers(0, 300, 64)
-    assert ix.plan(64, 16)["kernel"] == "kb256"
+    assert ix.plan(64, 16)["kernel"] == name
     s, r = [t.cpu().numpy() for t in ix.query(base[pick], 16)]
     ix.close()
     np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(16)[None, :])
