@@ -2078,7 +2078,7 @@ __global__ __launch_bounds__(64) void merge_kernel(const uint64_t* __restrict__ 
 // Threshold seed: k-th largest of the G sampled group maxima of each query. Group maxima are
 // scores of distinct corpus rows, so the result is a valid lower bound of the query's final
 // k-th best score.
-constexpr int kSampleMax = 16384;              // sampled rows
+constexpr int kSampleMax = 65536;              // sampled rows
 constexpr int kGroupMax = kSampleMax / 16;        // group maxima per query
 
 // One wave per query: the k-th largest ordered value is found bit by bit from the MSB
@@ -3032,9 +3032,11 @@ constexpr int kResidentSlots128 = 256 * 2;
 // larger corpus wants a larger sample: S = 16384 from 512k rows on (5M x 768: tile kernel 8.87 vs
 // 9.10 ms at S = 8192, the pre-pass 49 vs 30 us; 625k: kb256 1.03 vs 1.06 ms, 312k: a wash),
 // 8192 below (C2, 90k rows: 16384 measured +12 us end to end).
+// From 2M rows S = 32768 (5M x 768, kb256: 7.41 vs 7.63 ms per batch; 2.5M: 3.80 vs 3.87 ms;
+// 65536: the pre-pass grows to 173 us and eats the gain; 1.25M and 625k: 16384 stays ahead).
 inline int sample_rows_for(const ahr_index* ix) {
   if (ix->sample_rows >= 0) return ix->sample_rows;
-  return ix->count >= (1 << 19) ? 16384 : 8192;
+  return ix->count >= (1 << 21) ? 32768 : (ix->count >= (1 << 19) ? 16384 : 8192);
 }
 
 bool qkv_ok(const ahr_index* ix, int B, int k) {
@@ -3808,7 +3810,7 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum, int* n_calls) {
 int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   if (rows < -1 || rows > kSampleMax || (rows > 0 && ((rows & (rows - 1)) || rows < 256)))
-    return fail(AHR_EINVAL, "sample rows must be -1 (automatic), 0 or a power of two in [256, 16384]");
+    return fail(AHR_EINVAL, "sample rows must be -1 (automatic), 0 or a power of two in [256, 65536]");
   ix->sample_rows = rows;
   return AHR_OK;
 }

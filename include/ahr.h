@@ -100,8 +100,8 @@ int ahr_index_read(const ahr_index* ix, int64_t start, int64_t n, float* out, vo
 int ahr_index_profile_begin(ahr_index* ix, int max_calls);
 int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_calls);
 
-/* Rows scored by the threshold pre-pass: -1 = automatic (default: 8192, 16384 from 512k rows on),
- * 0 disables it, else a power of two in [256, 16384]. */
+/* Rows scored by the threshold pre-pass: -1 = automatic (default: 8192; 16384 from 512k, 32768 from 2M rows),
+ * 0 disables it, else a power of two in [256, 65536]. */
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
 
 /* Ablation switches for profiling, never set in production. Correct results: 8 = always the
