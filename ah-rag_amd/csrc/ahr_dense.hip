@@ -2082,7 +2082,11 @@ constexpr int kSampleMax = 65536;              // sampled rows
 constexpr int kGroupMax = kSampleMax / 16;        // group maxima per query
 
 // One wave per query: the k-th largest ordered value is found bit by bit from the MSB
-// (largest t with #{v >= t} >= k), one counting pass per bit over <= 16 values per lane.
+// (largest t with #{v >= t} >= k), one counting pass per bit over NJ values per lane (S <= 64 NJ
+// group maxima; the launch picks the smallest NJ: register arrays sized for the largest sample
+// made the S = 512 case of the 90k corpus pay 64 guarded loads and ballots per bit, 39 vs 24 us
+// for the pre-pass stage at C2).
+template <int NJ>
 __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict__ scores, int S,
                                                         int k, float* __restrict__ thr) {
   const int q = blockIdx.x;
@@ -2090,15 +2094,15 @@ __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict_
   const float* src = scores + (int64_t)q * S;
   // all loads in flight at once (clamped addresses, masked after): a per-lane guard around each
   // load serialised them, one memory latency per 64 values
-  float raw[kGroupMax / 64];
+  float raw[NJ];
 #pragma unroll
-  for (int j = 0; j < kGroupMax / 64; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int i = lane + 64 * j;
-    raw[j] = 64 * j < S ? src[i < S ? i : S - 1] : 0.f;  // 64 j < S is wave-uniform
+    raw[j] = src[i < S ? i : S - 1];
   }
-  uint32_t v[kGroupMax / 64];
+  uint32_t v[NJ];
 #pragma unroll
-  for (int j = 0; j < kGroupMax / 64; ++j) v[j] = lane + 64 * j < S ? ord_f32(raw[j]) : 0u;
+  for (int j = 0; j < NJ; ++j) v[j] = lane + 64 * j < S ? ord_f32(raw[j]) : 0u;
   // 20 bits from the MSB (sign, exponent, 11 mantissa bits): ans is the largest 20-bit prefix
   // with #{v >= ans} >= k, so ans <= the k-th largest value: a valid, ~5e-4-relative bound.
   uint32_t ans = 0;
@@ -2107,11 +2111,21 @@ __global__ __launch_bounds__(64) void sample_kth_kernel(const float* __restrict_
     // count over the wave with ballots: scalar popcounts, no cross-lane data movement
     int c = 0;
 #pragma unroll
-    for (int j = 0; j < kGroupMax / 64; ++j)
-      if (64 * j < S) c += __builtin_popcountll(__ballot(v[j] >= cand));  // S is wave-uniform
+    for (int j = 0; j < NJ; ++j) c += __builtin_popcountll(__ballot(v[j] >= cand));
     if (c >= k) ans = cand;
   }
   if (lane == 0) thr[q] = unord_f32(ans);
+}
+
+void launch_sample_kth(const float* scores, int B, int G, int k, float* thr, hipStream_t s) {
+  if (G <= 8 * 64)
+    hipLaunchKernelGGL(sample_kth_kernel<8>, dim3(B), dim3(64), 0, s, scores, G, k, thr);
+  else if (G <= 16 * 64)
+    hipLaunchKernelGGL(sample_kth_kernel<16>, dim3(B), dim3(64), 0, s, scores, G, k, thr);
+  else if (G <= 32 * 64)
+    hipLaunchKernelGGL(sample_kth_kernel<32>, dim3(B), dim3(64), 0, s, scores, G, k, thr);
+  else
+    hipLaunchKernelGGL(sample_kth_kernel<kGroupMax / 64>, dim3(B), dim3(64), 0, s, scores, G, k, thr);
 }
 
 // k-way merge when each lane holds one whole list in registers (n_lists <= 64, k_in <= KCAP):
@@ -3408,7 +3422,7 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     const int G = S / 16;  // 16-row groups
     launch_tile<DT, 8, MODE_GROUPMAX>(ix, S / kTileRows, (int)cdiv(B, kTileQ), 1, S / kTileRows, S, B, k, 0,
                                       nullptr, scores, G, 0, s);
-    hipLaunchKernelGGL(sample_kth_kernel, dim3(B), dim3(64), 0, s, scores, G, k, t);
+    launch_sample_kth(scores, B, G, k, t, s);
     thr = t;
   }
   prof_mark(ix, 2, s);
