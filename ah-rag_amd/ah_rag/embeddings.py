@@ -69,9 +69,16 @@ class HashEncoder:
 def load_encoder(model_name: str = DEFAULT_MODEL, dim: Optional[int] = None):
     """SentenceTransformer(model_name) when importable and cached, else HashEncoder.
 
-    Set AHR_ENCODER=hash to force the stand-in (benchmarks use synthetic vectors anyway).
+    AHR_ENCODER=hash forces the stand-in (benchmarks use synthetic vectors anyway);
+    AHR_ENCODER=torch runs the model's architecture as a batched bf16 PyTorch forward on the GPU
+    (ah_rag.encoder.TorchEncoder: a local checkpoint directory if `model_name` is one, else seeded
+    random weights).
     """
-    if os.environ.get("AHR_ENCODER", "").lower() != "hash":
+    mode = os.environ.get("AHR_ENCODER", "").lower()
+    if mode == "torch":
+        from .encoder import torch_encoder
+        return torch_encoder(model_name)
+    if mode != "hash":
         try:
             from sentence_transformers import SentenceTransformer  # type: ignore
 

@@ -674,8 +674,14 @@ class HierarchicalGraph:
         model_name = model_name or vi.get("model", DEFAULT_MODEL)
         engine = self.search_engine(db_path)
         if query_vectors is None:
-            query_vectors = self._encoder(model_name).encode(list(queries), normalize_embeddings=True)
-        q = torch.from_numpy(np.ascontiguousarray(np.asarray(query_vectors, np.float32)))
+            enc = self._encoder(model_name)
+            # a GPU encoder hands its [B, d] fp32 output over on the device (no host round trip)
+            extra = {"convert_to_tensor": True} if getattr(enc, "on_device", False) else {}
+            query_vectors = enc.encode(list(queries), normalize_embeddings=True, **extra)
+        if isinstance(query_vectors, torch.Tensor):
+            q = query_vectors.to(torch.float32)
+        else:
+            q = torch.from_numpy(np.ascontiguousarray(np.asarray(query_vectors, np.float32)))
         if q.dim() == 1:
             q = q.unsqueeze(0)
         rows, scores, res = engine.run(q, params)
