@@ -74,7 +74,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-f32-line", action="store_true",
                     help="N=1 hotpot90k: skip the exact-mode (fp32 index) line beside the bf16 headline")
     ap.add_argument("--inflight", type=int, default=2,
-                    help="batches in flight (one stream + index workspace each); rows-sharded runs use 1")
+                    help="batches in flight (one stream + index workspace each)")
     ap.add_argument("--recall-queries", type=int, default=256)
     ap.add_argument("--debug-flags", type=int, default=0,
                     help="ablation/kernel-selection switches (DenseIndex.set_debug_flags); 0 in production")
@@ -301,11 +301,13 @@ def run(args) -> None:
     # so the latency-bound stages of one batch (query conversion, pre-pass k-th selection, merge,
     # launch gaps) overlap the neighbouring batch's tile kernel. Every batch still runs the whole
     # path; only the order of independent batches' kernels on the GPU changes.
-    inflight = 1 if sharded else max(1, args.inflight)
+    # Row-sharded runs pipeline the same way: batch i's RCCL all-gather and merge overlap batch
+    # i + 1's local search (the collective is ordered after the work of the batch's stream).
+    inflight = max(1, args.inflight)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(inflight - 1)]
     outs = [(torch.empty((B, k), dtype=torch.float32, device=dev), torch.empty((B, k), dtype=torch.int32, device=dev))
             for _ in range(inflight)]
-    keys = torch.empty((B, k), dtype=torch.int64, device=dev)
+    keys = [torch.empty((B, k), dtype=torch.int64, device=dev) for _ in range(inflight)]
     for i in range(inflight):
         local.set_workspace(i)
         local.reserve(B, k)
@@ -315,12 +317,12 @@ def run(args) -> None:
     counter = [0]
 
     def step(depth: int):
-        if sharded:  # local top-k -> RCCL all-gather over xGMI -> device merge
-            return index.query(q, k, out_keys=keys)
         i = counter[0] % depth
         counter[0] += 1
         local.set_workspace(i)
         with torch.cuda.stream(streams[i]):  # current stream = the batch's stream: no cross-stream wait
+            if sharded:  # local top-k -> RCCL all-gather over xGMI -> device merge
+                return index.query(q, k, out_keys=keys[i])
             return local.query(q, k, out=outs[i])
 
     def timed(depth: int) -> float:

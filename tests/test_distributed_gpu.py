@@ -42,6 +42,25 @@ ref.upsert(C)
 s2, r2 = ref.query(Q, 10)
 assert torch.equal(r.cpu(), r2.cpu()), "rows differ"
 assert torch.equal(s.cpu(), s2.cpu()), "scores differ"
+# two batches in flight (bench.py's pipelined sharded step): a stream and a workspace each, the
+# collective of one batch beside the local search of the next
+streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)]
+kb = [torch.empty((100, 10), dtype=torch.int64, device=dev) for _ in range(2)]
+for i in range(2):
+    idx.local.set_workspace(i)
+    idx.reserve(100, 10)
+streams[1].wait_stream(streams[0])
+Qd = torch.from_numpy(Q).to(dev)
+outs = []
+for j in range(6):
+    i = j % 2
+    idx.local.set_workspace(i)
+    with torch.cuda.stream(streams[i]):
+        outs.append(idx.query(Qd, 10, out_keys=kb[i]))
+torch.cuda.synchronize()
+idx.local.set_workspace(0)
+for s3, r3 in outs:
+    assert torch.equal(r3.cpu(), r2.cpu()) and torch.equal(s3.cpu(), s2.cpu()), "pipelined batch differs"
 g = all_gather_keys(torch.arange(12, dtype=torch.int64, device=dev).view(3, 4))
 assert g.shape == (1, 3, 4) and g.is_cuda and torch.equal(g[0].cpu(), torch.arange(12).view(3, 4))
 torch.cuda.synchronize()
