@@ -636,6 +636,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
   // to the column's stash, one per set bit of a pass mask in a divergent loop.
   float* slot = reinterpret_cast<float*>(smem + kOffBuf1) + tid * 16;
   auto screen_tile = [&](int r0) __attribute__((always_inline)) {
+    const bool full = r0 + kTileRows <= n_rows;  // wave-uniform: row bound tests only on a ragged tile
     uint32_t gmask = 0;
 #pragma unroll
     for (int bj = 0; bj < 2; ++bj)
@@ -677,10 +678,12 @@ __global__ __launch_bounds__(kThreads, 2) void topk_tilelane_kernel(
         for (int c4 = 0; c4 < 4; ++c4) {
           const f32x4 v4 = *reinterpret_cast<const f32x4*>(slot + 4 * c4);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * c4 + e;
-            pm |= (v4[e] >= th && rb + (r & 3) + 8 * (r >> 2) < n_rows ? 1u : 0u) << r;
-          }
+          for (int e = 0; e < 4; ++e) pm |= (v4[e] >= th ? 1u : 0u) << (4 * c4 + e);
+        }
+        if (!full) {  // the ragged last tile only: drop rows past the corpus end
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (rb + (r & 3) + 8 * (r >> 2) >= n_rows) pm &= ~(1u << r);
         }
         while (pm) {
           const int r = __builtin_ctz(pm);
@@ -1639,6 +1642,7 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
       if (flags & kFlagSkipEpilogue) continue;
       // ---- tile end: (query slot nb, row half mh) groups = acc[4 mh .. 4 mh + 3][nb], 16 rows
       const int r0 = tile * kb256::kTR + wm * 128;
+      const bool full = tile * kb256::kTR + kb256::kTR <= n_rows;  // row bound tests only on a ragged tile
       uint32_t gmask = 0;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb)
@@ -1665,8 +1669,12 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
 #pragma unroll
           for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              pm |= (acc[4 * mh + u][nb][i] >= thr[nb] && rb + 16 * u + i < n_rows ? 1u : 0u) << (4 * u + i);
+            for (int i = 0; i < 4; ++i) pm |= (acc[4 * mh + u][nb][i] >= thr[nb] ? 1u : 0u) << (4 * u + i);
+          if (!full) {  // the ragged last tile only
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (rb + 16 * (r >> 2) + (r & 3) >= n_rows) pm &= ~(1u << r);
+          }
           while (pm) {
             const int r = __builtin_ctz(pm);
             pm &= pm - 1;
