@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "ahr_abi_version", "ahr_last_error", "ahr_device_count",
     "ahr_index_create", "ahr_index_destroy", "ahr_index_upsert", "ahr_index_truncate",
     "ahr_index_count", "ahr_index_info", "ahr_index_rows", "ahr_index_read", "ahr_index_reserve",
-    "ahr_index_profile_begin", "ahr_index_profile_end", "ahr_index_set_sample_rows", "ahr_index_plan",
+    "ahr_index_profile_begin", "ahr_index_profile_end", "ahr_index_set_sample_rows", "ahr_index_set_seed", "ahr_index_probe_seed", "ahr_index_plan",
     "ahr_index_set_debug_flags", "ahr_index_set_workspace",
     "ahr_index_query", "ahr_index_query_keys", "ahr_index_scores", "ahr_topk_merge", "ahr_key_decode",
     "ahr_graph_create", "ahr_graph_destroy", "ahr_graph_expand_rerank", "ahr_graph_expand",
@@ -98,6 +98,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_index_profile_begin": ([_P, _I], _I),
         "ahr_index_profile_end": ([_P, _P, _P], _I),
         "ahr_index_set_sample_rows": ([_P, _I], _I),
+        "ahr_index_set_seed": ([_P, _P], _I),
+        "ahr_index_probe_seed": ([_P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
         "ahr_index_plan": ([_P, _I, _I, _P, _P, _P, _P], _I),
     "ahr_index_set_workspace": ([_P, _I], _I),
         "ahr_index_set_debug_flags": ([_P, _I], _I),

@@ -127,9 +127,14 @@ class DenseIndex:
         nat.check(nat.lib().ahr_index_create(self.dim, code, self.capacity, self.device.index,
                                              nat.ctypes.byref(h)), "ahr_index_create")
         self._h = h
+        self._seed = None       # caller's admission thresholds (set_seed)
+        self._clusters = None   # cluster-probe seeding state (build_clusters)
 
     # -- lifecycle ---------------------------------------------------------------------------
     def close(self) -> None:
+        if getattr(self, "_clusters", None) is not None:
+            self._clusters["index"].close()
+            self._clusters = None
         if getattr(self, "_h", None) is not None and self._h.value:
             nat.lib().ahr_index_destroy(self._h)
             self._h = nat.ctypes.c_void_p()
@@ -190,10 +195,92 @@ class DenseIndex:
         """Query workspace (0..3) for the following queries: batches in flight on different
         streams must use different workspaces (include/ahr.h ahr_index_set_workspace)."""
         nat.check(nat.lib().ahr_index_set_workspace(self._h, int(slot)), "ahr_index_set_workspace")
+        if self._clusters is not None:  # the centroid search runs inside every seeded query
+            self._clusters["index"].set_workspace(slot)
 
     def reserve(self, max_batch: int, max_k: int = nat.AHR_MAX_K) -> None:
         with torch.cuda.device(self.device):
             nat.check(nat.lib().ahr_index_reserve(self._h, int(max_batch), int(max_k)), "ahr_index_reserve")
+        if self._clusters is not None:
+            self._clusters["index"].reserve(max_batch, self.PROBE_CLUSTERS)
+
+    # -- cluster-probe seeds (the tile kernels' admission threshold) --------------------------
+    PROBE_CLUSTERS = 8  # nearest clusters offered to the probe per query
+    PROBE_MIN_ROWS = 64  # the probe stops walking clusters once it holds this many rows
+
+    def build_clusters(self, n_clusters: Optional[int] = None, iters: int = 4, seed: int = 7) -> dict:
+        """Coarse clusters of the stored rows, so that query() (B > 16, k <= 16, bf16/f16) seeds the
+        fused kernels from each query's nearest clusters (ahr_index_probe_seed: the exact k-th best
+        over those rows, less a rounding bound) instead of the sampled pre-pass. Spherical k-means:
+        random member rows as initial centroids, assignment by this library's fused top-1 against
+        a centroid index of the same dtype, centroids = normalised member means. Upserts and
+        truncation after the build leave every seed valid (new rows are simply not probed); call
+        again to refresh. Returns {"clusters", "rows", "empty"}."""
+        if self.dtype == "f32":
+            raise ValueError("cluster-probe seeds need a bf16 / f16 index")
+        n = len(self)
+        C = int(n_clusters or max(16, n // 22))
+        if n < 2 * C:
+            raise ValueError("too few rows for that many clusters")
+        X = self.read()
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        cent = torch.nn.functional.normalize(X[torch.randperm(n, generator=g)[:C].to(self.device)], dim=1)
+        cidx = DenseIndex(self.dim, C, dtype=self.dtype, device=self.device)
+        asg = torch.empty(n, dtype=torch.int64, device=self.device)
+        for it in range(iters + 1):
+            cidx.upsert(cent, start=0)
+            for s0 in range(0, n, 1 << 18):
+                asg[s0:s0 + (1 << 18)] = cidx.query(X[s0:s0 + (1 << 18)], 1)[1][:, 0].long()
+            if it == iters:
+                break
+            acc = torch.zeros_like(cent).index_add_(0, asg, X)
+            cnt = torch.bincount(asg, minlength=C)
+            keep = cnt > 0
+            cent[keep] = torch.nn.functional.normalize(acc[keep], dim=1)
+        cnt = torch.bincount(asg, minlength=C)
+        off = torch.zeros(C + 1, dtype=torch.int64, device=self.device)
+        off[1:] = torch.cumsum(cnt, 0)
+        rows = torch.argsort(asg, stable=True).to(torch.int32).contiguous()
+        if self._clusters is not None:
+            self._clusters["index"].close()
+        self._clusters = {"index": cidx, "off": off, "rows": rows, "C": C}
+        del X
+        return {"clusters": C, "rows": n, "empty": int((cnt == 0).sum())}
+
+    def drop_clusters(self) -> None:
+        if self._clusters is not None:
+            self._clusters["index"].close()
+        self._clusters = None
+
+    def _probe_seed(self, q: torch.Tensor, k: int, normalize: bool, stream) -> Optional[torch.Tensor]:
+        """Device thresholds [B] from the query's nearest clusters (None: this call takes the
+        sampled pre-pass: no clusters, the small-batch kernels, k > 16)."""
+        c = self._clusters
+        B = q.shape[0]
+        if c is None or B <= 16 or k > 16:
+            return None
+        keys = c["index"].query_keys(q, self.PROBE_CLUSTERS, normalize=normalize, stream=stream)
+        thr = torch.empty((B,), dtype=torch.float32, device=self.device)
+        _on_stream(stream, self.device, thr)
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_index_probe_seed(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
+                                                     nat.ptr(keys), self.PROBE_CLUSTERS, nat.ptr(c["off"]),
+                                                     nat.ptr(c["rows"]), self.PROBE_MIN_ROWS, nat.ptr(thr),
+                                                     nat.stream_ptr(stream)), "ahr_index_probe_seed")
+        if stream is not None:
+            keys.record_stream(stream)
+        return thr
+
+    def _seeded(self, q: torch.Tensor, k: int, normalize: bool, stream, launch) -> None:
+        thr = self._probe_seed(q, k, normalize, stream)
+        if thr is None:
+            launch()
+            return
+        nat.check(nat.lib().ahr_index_set_seed(self._h, nat.ptr(thr)), "ahr_index_set_seed")
+        try:
+            launch()
+        finally:  # back to the caller's seed (or the pre-pass)
+            nat.check(nat.lib().ahr_index_set_seed(self._h, nat.ptr(self._seed)), "ahr_index_set_seed")
 
     def read(self, start: int = 0, n: Optional[int] = None) -> torch.Tensor:
         """Stored rows decoded to fp32 [n, dim] on the device (after dtype rounding)."""
@@ -209,6 +296,16 @@ class DenseIndex:
     def set_sample_rows(self, rows: int) -> None:
         """Rows scored by the threshold pre-pass (0 disables it)."""
         nat.check(nat.lib().ahr_index_set_sample_rows(self._h, int(rows)), "ahr_index_set_sample_rows")
+
+    def set_seed(self, thr: Optional[torch.Tensor]) -> None:
+        """Admission thresholds for the next queries (device fp32 [>= B], one valid lower bound of
+        each query's k-th best score), replacing the sampled pre-pass; None restores it. The
+        tensor must stay alive while queries use it."""
+        if thr is not None:
+            if not (thr.is_cuda and thr.dtype == torch.float32 and thr.is_contiguous()):
+                raise ValueError("seed must be a contiguous float32 device tensor")
+        self._seed = thr
+        nat.check(nat.lib().ahr_index_set_seed(self._h, nat.ptr(thr)), "ahr_index_set_seed")
 
     def set_debug_flags(self, flags: int) -> None:
         """Ablation switches (include/ahr.h): 2 = skip the top-k epilogue (garbage results),
@@ -262,9 +359,9 @@ class DenseIndex:
             scores, rows = out
         _on_stream(stream, self.device, q, scores, rows)
         with torch.cuda.device(self.device):
-            nat.check(nat.lib().ahr_index_query(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
-                                                nat.ptr(scores), nat.ptr(rows), nat.stream_ptr(stream)),
-                      "ahr_index_query")
+            self._seeded(q, k, normalize, stream, lambda: nat.check(
+                nat.lib().ahr_index_query(self._h, nat.ptr(q), B, int(k), int(bool(normalize)), nat.ptr(scores),
+                                          nat.ptr(rows), nat.stream_ptr(stream)), "ahr_index_query"))
         return scores, rows
 
     def scores(self, queries: ArrayLike, normalize: bool = False,
@@ -289,9 +386,9 @@ class DenseIndex:
         keys = out if out is not None else torch.empty((B, k), dtype=torch.int64, device=self.device)
         _on_stream(stream, self.device, q, keys)
         with torch.cuda.device(self.device):
-            nat.check(nat.lib().ahr_index_query_keys(self._h, nat.ptr(q), B, int(k), int(bool(normalize)),
-                                                     int(row_base), nat.ptr(keys), nat.stream_ptr(stream)),
-                      "ahr_index_query_keys")
+            self._seeded(q, k, normalize, stream, lambda: nat.check(
+                nat.lib().ahr_index_query_keys(self._h, nat.ptr(q), B, int(k), int(bool(normalize)), int(row_base),
+                                               nat.ptr(keys), nat.stream_ptr(stream)), "ahr_index_query_keys"))
         return keys
 
 

@@ -2937,6 +2937,162 @@ __global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __rest
   }
 }
 
+// Cluster-probe seed (ahr_index_probe_seed): per query, the exact scores of the rows of its
+// nearest clusters (cluster ids from a centroid search, packed keys [B][P]), walked in order until
+// at least min_rows rows are gathered; the seed is the k-th largest per-row LOWER BOUND of the
+// score the fused kernels compute for that row: score - err, err = sum |q_i c_i| * (2^-8 for bf16
+// storage / 2^-10 for f16: the kernels score the storage-rounded query, this kernel the fp32 one;
+// + dim * 2^-23: two fp32 summation orders). Any k real rows give a valid lower bound of the final
+// k-th best, so the seed admits every true top-k row; with clusters that hold the query's
+// neighbours it sits just under the k-th best (~10 survivors per query at C2 instead of ~110 from
+// the sampled pre-pass). Fewer than k rows gathered: -inf (no pruning for that query).
+// One 256-thread workgroup per query: the fp32 query in LDS, 4 rows per wave in flight.
+constexpr int kProbeMaxRows = 256;
+constexpr int kProbeMaxDim = 1024;
+
+__global__ __launch_bounds__(256) void probe_seed_kernel(const uint8_t* __restrict__ corpus, int64_t row_stride, int dt,
+                                                         int dim, int64_t n_rows, const float* __restrict__ qsrc,
+                                                         int normalize, const uint64_t* __restrict__ ckeys, int P,
+                                                         const int64_t* __restrict__ list_off,
+                                                         const int32_t* __restrict__ list_rows, int min_rows, int k,
+                                                         float* __restrict__ thr) {
+  __shared__ float qs[kProbeMaxDim];
+  __shared__ int32_t cand[kProbeMaxRows];
+  __shared__ float lb[kProbeMaxRows];
+  __shared__ float red[4];
+  __shared__ int n_cand;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const float* x = qsrc + (int64_t)b * dim;
+  float ss = 0.f;
+  for (int j = tid; j < kProbeMaxDim; j += 256) {
+    const float v = j < dim ? x[j] : 0.f;
+    qs[j] = v;
+    ss = fmaf(v, v, ss);
+  }
+  if (normalize) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    if (lane == 0) red[wave] = ss;
+  }
+  // the nearest clusters' list ranges (wave 0, lane j = cluster j; P <= 64), taken in order while
+  // fewer than min_rows rows are held, then copied by all threads (slots past the row count -> -1)
+  __shared__ int64_t cl_off[64];
+  __shared__ int cl_start[65];
+  if (wave == 0) {
+    int64_t o0 = 0;
+    int nj = 0;
+    if (lane < P) {
+      const uint64_t key = ckeys[(int64_t)b * P + lane];
+      if (key) {
+        const int c = (int)key_row(key);
+        o0 = list_off[c];
+        nj = (int)(list_off[c + 1] - o0);
+      }
+    }
+    int incl = nj;  // inclusive prefix sum over the lanes
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    const int excl = incl - nj;
+    const bool take = lane < P && excl < min_rows;
+    const int start = take ? (excl < kProbeMaxRows ? excl : kProbeMaxRows) : kProbeMaxRows;
+    if (lane < 64) {
+      cl_off[lane] = o0;
+      cl_start[lane] = start;
+    }
+    // rows held: the taken clusters' total, capped
+    const uint64_t tk = __ballot(take);
+    const int last = tk ? 63 - __builtin_clzll(tk) : -1;
+    const int total = last >= 0 ? __shfl(incl, last, 64) : 0;
+    if (lane == 0) {
+      cl_start[64] = total < kProbeMaxRows ? total : kProbeMaxRows;
+      n_cand = cl_start[64];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n_cand; i += 256) {
+    int j = 0;
+    while (j + 1 < 64 && cl_start[j + 1] <= i) ++j;  // clusters are few and in order
+    const int32_t r = list_rows[cl_off[j] + (i - cl_start[j])];
+    cand[i] = (r >= 0 && r < n_rows) ? r : -1;
+  }
+  __syncthreads();
+  if (normalize) {
+    const float inv = 1.0f / fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
+    for (int j = tid; j < dim; j += 256) qs[j] *= inv;
+    __syncthreads();
+  }
+  const int n = n_cand;
+  const float rel = (dt == DT_BF16 ? 0x1p-8f : 0x1p-10f) + (float)dim * 0x1p-23f;
+  // each lane covers dims 4 lane + 256 u (u < 4), 4 half values (8 B) per load
+  for (int i0 = wave * 4; i0 < n; i0 += 16) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
+    uint2 raw[4][4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = i0 + rr < n ? i0 + rr : i0;
+      const uint8_t* row = corpus + (int64_t)(cand[i] < 0 ? 0 : cand[i]) * row_stride;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = 4 * lane + 256 * u;
+        raw[rr][u] = j < dim ? *reinterpret_cast<const uint2*>(row + 2 * j) : make_uint2(0, 0);
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = 4 * lane + 256 * u;
+        const uint32_t w[2] = {raw[rr][u].x, raw[rr][u].y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint16_t h = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+          const float c = dt == DT_BF16 ? __uint_as_float((uint32_t)h << 16)
+                                        : (float)__builtin_bit_cast(_Float16, h);
+          const float qv = j + e < dim ? qs[j + e] : 0.f;
+          s[rr] = fmaf(qv, c, s[rr]);
+          a[rr] = fmaf(fabsf(qv), fabsf(c), a[rr]);
+        }
+      }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        s[rr] += __shfl_xor(s[rr], off, 64);
+        a[rr] += __shfl_xor(a[rr], off, 64);
+      }
+      if (lane == 0 && i0 + rr < n) lb[i0 + rr] = cand[i0 + rr] < 0 ? -INFINITY : s[rr] - a[rr] * rel;
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  if (n < k) {
+    if (lane == 0) thr[b] = -INFINITY;
+    return;
+  }
+  // k-th largest lower bound: the largest 20-bit ordered prefix with >= k values at or above it
+  uint32_t v[kProbeMaxRows / 64];
+#pragma unroll
+  for (int u = 0; u < kProbeMaxRows / 64; ++u) {
+    const int i = lane + 64 * u;
+    v[u] = i < n ? ord_f32(lb[i]) : 0u;
+  }
+  uint32_t ans = 0;
+  for (int bit = 31; bit >= 12; --bit) {
+    const uint32_t cand_v = ans | (1u << bit);
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < kProbeMaxRows / 64; ++u) c += __builtin_popcountll(__ballot(v[u] >= cand_v));
+    if (c >= k) ans = cand_v;
+  }
+  if (lane == 0) thr[b] = unord_f32(ans);
+}
+
 }  // namespace dense
 }  // namespace ahr
 
@@ -2982,6 +3138,7 @@ struct ahr_index {
   uint8_t* cand = nullptr;  // query-resident kernel: candidate groups (counts, row bases, scores)
   int64_t cand_cap = 0;     // bytes
   int sample_rows = -1;     // S; 0 disables the threshold pre-pass, -1 = sample_rows_for(count)
+  const float* seed = nullptr;  // caller-supplied admission thresholds [B] (device), replace the pre-pass
   // The fields above (qbuf .. cand_cap) are the ACTIVE query workspace; the others are parked
   // here (ahr_index_set_workspace swaps them) so batches on different streams never share one.
   ahr_query_ws parked[kMaxWorkspaces];
@@ -3423,7 +3580,9 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     }
   }
   const int S = sample_rows_for(ix);
-  if (S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
+  if (ix->seed) {
+    thr = ix->seed;  // the caller's valid lower bounds of each query's k-th best score
+  } else if (S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
     // Threshold pre-pass: score the first S rows, take each query's k-th best.
     float* scores = ix->sample;
     float* t = ix->sample + (int64_t)B * (S / 16);
@@ -3834,6 +3993,29 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows) {
   if (rows < -1 || rows > kSampleMax || (rows > 0 && ((rows & (rows - 1)) || rows < 256)))
     return fail(AHR_EINVAL, "sample rows must be -1 (automatic), 0 or a power of two in [256, 65536]");
   ix->sample_rows = rows;
+  return AHR_OK;
+}
+
+int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normalize_q, const uint64_t* cluster_keys,
+                         int P, const int64_t* list_off, const int32_t* list_rows, int min_rows, float* thr,
+                         void* stream) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  if (B < 0 || k <= 0 || P <= 0 || min_rows <= 0) return fail(AHR_EINVAL, "B >= 0, k, P, min_rows > 0 required");
+  if (ix->dtype == AHR_F32) return fail(AHR_EUNSUP, "cluster probe seeds: bf16 / f16 indexes");
+  if (ix->dim > kProbeMaxDim || k > kProbeMaxRows) return fail(AHR_EUNSUP, "dim <= 1024 and k <= 256");
+  if (B == 0) return AHR_OK;
+  if (!q || !cluster_keys || !list_off || !list_rows || !thr) return fail(AHR_EINVAL, "null buffer");
+  DeviceGuard dg(ix->device);
+  hipLaunchKernelGGL(probe_seed_kernel, dim3((unsigned)B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     ix->rows, ix->row_stride, ix->dtype, ix->dim, ix->count, q, normalize_q, cluster_keys, P,
+                     list_off, list_rows, std::min(min_rows, kProbeMaxRows), k, thr);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_index_set_seed(ahr_index* ix, const float* thr) {
+  if (!ix) return fail(AHR_EINVAL, "null index");
+  ix->seed = thr;
   return AHR_OK;
 }
 

@@ -103,6 +103,25 @@ int ahr_index_profile_end(ahr_index* ix, float* stage_ms_sum /* [4] */, int* n_c
 /* Rows scored by the threshold pre-pass: -1 = automatic (default: 8192; 16384 from 512k, 32768 from 2M rows),
  * 0 disables it, else a power of two in [256, 65536]. */
 int ahr_index_set_sample_rows(ahr_index* ix, int rows);
+/* Caller-supplied admission thresholds (device pointer to >= B floats, one per query of the next
+ * queries; NULL restores the built-in pre-pass). Each value must be a valid lower bound of that
+ * query's final k-th best score as this index computes it (e.g. the k-th best over any k rows,
+ * less a rounding margin): the fused kernels then skip the threshold pre-pass. B > 16 plans only
+ * (the small-batch kernels use no threshold). Replaces nothing in the reference (Chroma has no
+ * such knob); it is how a coarse-cluster probe seeds the exact search. */
+int ahr_index_set_seed(ahr_index* ix, const float* thr);
+
+/* Cluster-probe seeds for ahr_index_set_seed (bf16 / f16 indexes, dim <= 1024): per query b, the
+ * rows of clusters key_row(cluster_keys[b][0..P)) (the packed keys of a top-P search over the
+ * cluster centroids; 0 = none), taken from the CSR list_rows[list_off[c] .. list_off[c+1]) in
+ * order until min_rows rows, scored exactly in fp32 against the fp32 query (normalised if
+ * normalize_q); thr[b] = the k-th largest of score - err (err bounds the difference from the
+ * fused kernels' score of that row), or -inf when fewer than k rows exist. Slots >= the row
+ * count are skipped, so lists built before later upserts or truncation stay valid (a stale list
+ * only weakens the seed). All pointers are device pointers; stream-ordered. */
+int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normalize_q, const uint64_t* cluster_keys,
+                         int P, const int64_t* list_off, const int32_t* list_rows, int min_rows, float* thr,
+                         void* stream);
 
 /* Ablation switches for profiling, never set in production. Correct results: 8 = always the
  * 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile kernel at any
