@@ -2944,43 +2944,58 @@ __global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __rest
 // storage / 2^-10 for f16: the kernels score the storage-rounded query, this kernel the fp32 one;
 // + dim * 2^-23: two fp32 summation orders). Any k real rows give a valid lower bound of the final
 // k-th best, so the seed admits every true top-k row; with clusters that hold the query's
-// neighbours it sits just under the k-th best (~10 survivors per query at C2 instead of ~110 from
+// neighbours it sits just under the k-th best (~18 survivors per query at C2 instead of ~110 from
 // the sampled pre-pass). Fewer than k rows gathered: -inf (no pruning for that query).
-// One 256-thread workgroup per query: the fp32 query in LDS, 4 rows per wave in flight.
+// One 256-thread workgroup per query; every wave holds the fp32 query in registers (lane: dims
+// 4 lane + 256 u) and scores a quarter of the rows, kProbeBatch rows' loads in flight at once.
 constexpr int kProbeMaxRows = 256;
 constexpr int kProbeMaxDim = 1024;
+constexpr int kProbeBatch = 8;
 
-__global__ __launch_bounds__(256) void probe_seed_kernel(const uint8_t* __restrict__ corpus, int64_t row_stride, int dt,
-                                                         int dim, int64_t n_rows, const float* __restrict__ qsrc,
-                                                         int normalize, const uint64_t* __restrict__ ckeys, int P,
-                                                         const int64_t* __restrict__ list_off,
-                                                         const int32_t* __restrict__ list_rows, int min_rows, int k,
-                                                         float* __restrict__ thr) {
-  __shared__ float qs[kProbeMaxDim];
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, 0xf, false));
+}
+// wave64 sum by DPP row shifts + row broadcasts (as wave_max_u64); the result in every lane
+__device__ __forceinline__ float wave_sum_f32(float x) {
+  x += dpp_f32<0x111, 0xf>(x);
+  x += dpp_f32<0x112, 0xf>(x);
+  x += dpp_f32<0x114, 0xf>(x);
+  x += dpp_f32<0x118, 0xf>(x);
+  x += dpp_f32<0x142, 0xa>(x);
+  x += dpp_f32<0x143, 0xc>(x);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+__global__ __launch_bounds__(256, 2) void probe_seed_kernel(const uint8_t* __restrict__ corpus, int64_t row_stride,
+                                                            int dt, int dim, int64_t n_rows,
+                                                            const float* __restrict__ qsrc, int normalize,
+                                                            const uint64_t* __restrict__ ckeys, int P,
+                                                            const int64_t* __restrict__ list_off,
+                                                            const int32_t* __restrict__ list_rows, int min_rows,
+                                                            int k, float* __restrict__ thr) {
   __shared__ int32_t cand[kProbeMaxRows];
   __shared__ float lb[kProbeMaxRows];
-  __shared__ float red[4];
-  __shared__ int n_cand;
+  __shared__ int64_t cl_off[64];
+  __shared__ int cl_start[65];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  // the query, whole, in every wave's registers
   const float* x = qsrc + (int64_t)b * dim;
+  float qv[4][4];
   float ss = 0.f;
-  for (int j = tid; j < kProbeMaxDim; j += 256) {
-    const float v = j < dim ? x[j] : 0.f;
-    qs[j] = v;
-    ss = fmaf(v, v, ss);
-  }
-  if (normalize) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
-    if (lane == 0) red[wave] = ss;
-  }
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * lane + 256 * u + e;
+      qv[u][e] = j < dim ? x[j] : 0.f;
+      ss = fmaf(qv[u][e], qv[u][e], ss);
+    }
   // the nearest clusters' list ranges (wave 0, lane j = cluster j; P <= 64), taken in order while
-  // fewer than min_rows rows are held, then copied by all threads (slots past the row count -> -1)
-  __shared__ int64_t cl_off[64];
-  __shared__ int cl_start[65];
+  // fewer than min_rows rows are held
   if (wave == 0) {
     int64_t o0 = 0;
     int nj = 0;
@@ -3000,43 +3015,38 @@ __global__ __launch_bounds__(256) void probe_seed_kernel(const uint8_t* __restri
     }
     const int excl = incl - nj;
     const bool take = lane < P && excl < min_rows;
-    const int start = take ? (excl < kProbeMaxRows ? excl : kProbeMaxRows) : kProbeMaxRows;
-    if (lane < 64) {
-      cl_off[lane] = o0;
-      cl_start[lane] = start;
-    }
-    // rows held: the taken clusters' total, capped
+    cl_off[lane] = o0;
+    cl_start[lane] = take ? (excl < kProbeMaxRows ? excl : kProbeMaxRows) : kProbeMaxRows;
     const uint64_t tk = __ballot(take);
     const int last = tk ? 63 - __builtin_clzll(tk) : -1;
     const int total = last >= 0 ? __shfl(incl, last, 64) : 0;
-    if (lane == 0) {
-      cl_start[64] = total < kProbeMaxRows ? total : kProbeMaxRows;
-      n_cand = cl_start[64];
-    }
+    if (lane == 0) cl_start[64] = total < kProbeMaxRows ? total : kProbeMaxRows;
+  }
+  if (normalize) {
+    const float inv = 1.0f / fmaxf(sqrtf(wave_sum_f32(ss)), 1e-12f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qv[u][e] *= inv;
   }
   __syncthreads();
-  for (int i = tid; i < n_cand; i += 256) {
+  const int n = cl_start[64];
+  for (int i = tid; i < n; i += 256) {
     int j = 0;
     while (j + 1 < 64 && cl_start[j + 1] <= i) ++j;  // clusters are few and in order
     const int32_t r = list_rows[cl_off[j] + (i - cl_start[j])];
     cand[i] = (r >= 0 && r < n_rows) ? r : -1;
   }
   __syncthreads();
-  if (normalize) {
-    const float inv = 1.0f / fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
-    for (int j = tid; j < dim; j += 256) qs[j] *= inv;
-    __syncthreads();
-  }
-  const int n = n_cand;
   const float rel = (dt == DT_BF16 ? 0x1p-8f : 0x1p-10f) + (float)dim * 0x1p-23f;
-  // each lane covers dims 4 lane + 256 u (u < 4), 4 half values (8 B) per load
-  for (int i0 = wave * 4; i0 < n; i0 += 16) {
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
-    uint2 raw[4][4];
+  const int w_begin = wave * n / 4, w_end = (wave + 1) * n / 4;
+  for (int i0 = w_begin; i0 < w_end; i0 += kProbeBatch) {
+    uint2 raw[kProbeBatch][4];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int i = i0 + rr < n ? i0 + rr : i0;
-      const uint8_t* row = corpus + (int64_t)(cand[i] < 0 ? 0 : cand[i]) * row_stride;
+    for (int rr = 0; rr < kProbeBatch; ++rr) {
+      const int i = i0 + rr < w_end ? i0 + rr : i0;
+      const int32_t r = cand[i];
+      const uint8_t* row = corpus + (int64_t)(r < 0 ? 0 : r) * row_stride;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int j = 4 * lane + 256 * u;
@@ -3044,29 +3054,23 @@ __global__ __launch_bounds__(256) void probe_seed_kernel(const uint8_t* __restri
       }
     }
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
+    for (int rr = 0; rr < kProbeBatch; ++rr) {
+      float sc = 0.f, ab = 0.f;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int j = 4 * lane + 256 * u;
         const uint32_t w[2] = {raw[rr][u].x, raw[rr][u].y};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const uint16_t h = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
           const float c = dt == DT_BF16 ? __uint_as_float((uint32_t)h << 16)
                                         : (float)__builtin_bit_cast(_Float16, h);
-          const float qv = j + e < dim ? qs[j + e] : 0.f;
-          s[rr] = fmaf(qv, c, s[rr]);
-          a[rr] = fmaf(fabsf(qv), fabsf(c), a[rr]);
+          sc = fmaf(qv[u][e], c, sc);
+          ab = fmaf(fabsf(qv[u][e]), fabsf(c), ab);
         }
       }
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        s[rr] += __shfl_xor(s[rr], off, 64);
-        a[rr] += __shfl_xor(a[rr], off, 64);
-      }
-      if (lane == 0 && i0 + rr < n) lb[i0 + rr] = cand[i0 + rr] < 0 ? -INFINITY : s[rr] - a[rr] * rel;
+      sc = wave_sum_f32(sc);
+      ab = wave_sum_f32(ab);
+      if (lane == 0 && i0 + rr < w_end) lb[i0 + rr] = cand[i0 + rr] < 0 ? -INFINITY : sc - ab * rel;
     }
   }
   __syncthreads();

@@ -6,8 +6,9 @@ coarse-cluster probe computed with torch on the GPU (k-means centroids, the quer
 clusters, the exact k-th best score among their members minus a rounding margin) and is handed to
 the kernel through DenseIndex.set_seed (ahr_index_set_seed). Measures, per (clusters, probes):
 survivors per query (rows scoring >= the seed), the tile kernel's event-timed duration, and that
-the results equal the production path's. The probe itself is not timed (this bounds the gain a
-device probe could bring; it is not a product path).
+the results equal the production path's. The torch probe itself is not timed (this bounds the
+gain a device probe could bring). The second half times the product path (build_clusters ->
+ahr_index_probe_seed -> seeded kernels) end to end, and a library GEMM + topk centroid search.
 """
 import argparse
 import json
@@ -42,6 +43,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--clusters", default="1024,4096")
     ap.add_argument("--probes", default="1,2,4")
+    ap.add_argument("--probe-clusters", type=int, default=0, help="device path: nearest clusters per query (0: default)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c = SyntheticCorpus(HOTPOT_90K, dev)
@@ -102,6 +104,8 @@ def main():
         return (time.perf_counter() - t0) / steps * 1e3
     ix.drop_clusters()
     out["device_production_ms_per_batch"] = round(wall(lambda: ix.query(q, k)), 4)
+    if a.probe_clusters:
+        ix.PROBE_CLUSTERS = a.probe_clusters
     t0 = time.perf_counter()
     info = ix.build_clusters()
     torch.cuda.synchronize()
@@ -118,6 +122,11 @@ def main():
     out["device_centroid_search_prepass512_ms"] = round(wall(lambda: cl["index"].query_keys(q, ix.PROBE_CLUSTERS)), 4)
     out["device_probe_prepass512_ms_per_batch"] = round(wall(lambda: ix.query(q, k)), 4)
     cl["index"].set_sample_rows(-1)
+    # a library GEMM (hipBLASLt through torch) + torch.topk for the same centroid top-P
+    cent_bf = cl["index"].read().to(torch.bfloat16)
+    qb = q.to(torch.bfloat16)
+    out["library_centroid_gemm_topk_ms"] = round(wall(lambda: torch.topk(qb @ cent_bf.T, ix.PROBE_CLUSTERS, dim=1)), 4)
+    out["library_centroid_gemm_ms"] = round(wall(lambda: qb @ cent_bf.T), 4)
     thr = ix._probe_seed(q, k, False, None)
     out["device_probe_survivors_per_query"] = float((S >= thr[:, None]).sum(1).float().mean())
     out["device_probe_weak_queries"] = int((~torch.isfinite(thr)).sum())
