@@ -194,6 +194,8 @@ enum {
   kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
   kFlagNoKB256 = 262144,  // plan without the k-blocked kernels
   kFlagKB128 = 524288,    // the k-blocked 256x128 kernel wherever it applies (bf16/f16, k <= 16)
+  kFlagTileZero = 1 << 20,   // k-blocked kernels: every tile's operands read from tile 0 (L2-resident; wrong results)
+  kFlagTileFirst = 1 << 21,  // k-blocked kernels: every tile read from the split's first tile (wrong results)
 };
 constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
                              kFlagKB256 | kFlagNoKB256 | kFlagKB128;
@@ -1548,7 +1550,9 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
     // the workgroup's queries: rows (q0 & 255) .. + kTQ of each k-block of their 256-query tile
     const uint8_t* qblk = queries_kb + (q0 & 255) * kb256::kKB;
     auto issue = [&](int c, int stage) __attribute__((always_inline)) {
-      const int t = t_begin + c / n_kb;
+      int t = t_begin + c / n_kb;
+      if (flags & kFlagTileZero) t = 0;
+      if (flags & kFlagTileFirst) t = t_begin;
       const int kb = c % n_kb;
       const __amdgpu_buffer_rsrc_t a_rsrc =
           tile_rsrc(corpus_kb + kb256::block(t, kb, n_kb) * kb256::kBlock, kb256::kBlock);
@@ -4026,7 +4030,7 @@ int ahr_index_set_seed(ahr_index* ix, const float* thr) {
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
-                             kKernelFlags | kFlagSmallWide);
+                             kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst);
   return AHR_OK;
 }
 
