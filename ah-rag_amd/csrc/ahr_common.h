@@ -27,7 +27,9 @@ inline void ensure_lds_attr(std::atomic<uint64_t>& done, const void* fn, int byt
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const uint64_t bit = 1ull << (dev & 63);
   if (done.load(std::memory_order_acquire) & bit) return;
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  // a refused opt-in must not surface as the next call's hipGetLastError(): a launch that needs
+  // more LDS than the default then fails on its own and reports that
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) (void)hipGetLastError();
   done.fetch_or(bit, std::memory_order_acq_rel);
 }
 

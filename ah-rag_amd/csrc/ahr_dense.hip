@@ -196,6 +196,7 @@ enum {
   kFlagKB128 = 524288,    // the k-blocked 256x128 kernel wherever it applies (bf16/f16, k <= 16)
   kFlagTileZero = 1 << 20,   // k-blocked kernels: every tile's operands read from tile 0 (L2-resident; wrong results)
   kFlagTileFirst = 1 << 21,  // k-blocked kernels: every tile read from the split's first tile (wrong results)
+  kFlagNoFold = 1 << 22,     // small kernels: merge launch instead of the last-workgroup fold (A/B)
 };
 constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
                              kFlagKB256 | kFlagNoKB256 | kFlagKB128;
@@ -2543,6 +2544,88 @@ __global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restric
 }
 
 
+// One wave merges n_lists (<= 512) sorted lists of k_in keys held in LDS: k rounds of a DPP wave
+// max over the list heads (lane l owns lists l + 64 u), a head advancing by an LDS read, no
+// barrier per output; output j goes to o0 + j (merge_block_kernel and the small kernels' fold).
+__device__ __forceinline__ void walk_lists_lds(const uint64_t* kb, int n_lists, int k_in, int k, int64_t o0,
+                                               float* __restrict__ scores, int32_t* __restrict__ rows,
+                                               uint64_t* __restrict__ keys_out) {
+  const int lane = threadIdx.x & 63;
+  constexpr int kH = 8;  // n_lists <= 512
+  int ptr[kH];
+  uint64_t head[kH];
+#pragma unroll
+  for (int u = 0; u < kH; ++u) {
+    const int l = lane + 64 * u;
+    ptr[u] = 0;
+    head[u] = (l < n_lists && k_in > 0) ? kb[l * k_in] : 0;
+  }
+  uint64_t mine = 0;  // lane j % 64 keeps the j-th winner; flushed in windows of 64 outputs
+  for (int j = 0; j < k; ++j) {
+    uint64_t m = head[0];
+#pragma unroll
+    for (int u = 1; u < kH; ++u) m = max_u64(m, head[u]);
+    const uint64_t best = wave_max_u64(m);
+    if (best != 0 && m == best) {
+#pragma unroll
+      for (int u = 0; u < kH; ++u) {
+        if (head[u] == best) {
+          const int l = lane + 64 * u;
+          ++ptr[u];
+          head[u] = ptr[u] < k_in ? kb[l * k_in + ptr[u]] : 0;
+        }
+      }
+    }
+    if (lane == (j & 63)) mine = best;
+    if ((j & 63) == 63 || j == k - 1) {
+      const int j0 = j & ~63;
+      if (j0 + lane <= j) {
+        const int64_t o = o0 + j0 + lane;
+        if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
+        if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
+        if (keys_out) keys_out[o] = mine;
+      }
+    }
+  }
+}
+
+// Small-batch fold (B <= kFoldMaxQ): every workgroup of a small-batch launch publishes its
+// per-(query, split) lists and arrives on a counter in the query workspace; the LAST to arrive
+// merges the n_splits lists of each query (walk_lists_lds) and writes the outputs, so a single
+// search() is one launch instead of search + merge_block_kernel (the merge launch and its gap
+// were ~7 of ~35 us at B = 1). The counter is reset by that workgroup for the next launch on the
+// workspace. lds: n_q * n_splits * k_out keys (<= kFoldMaxLds), then the arrival flag (no static LDS: the small
+// kernel opts in to 160 KiB of dynamic LDS, which leaves none). Nothing waits: no workgroup depends on another's
+// progress, so there is no residency requirement.
+constexpr int kFoldMaxQ = 4;
+// all queries' lists in LDS at once; beyond 64 KiB the small kernel's workgroups could no longer
+// share a CU with the other batch in flight
+constexpr int kFoldMaxLds = 64 * 1024;
+__device__ __forceinline__ void fold_last_arrival(const uint64_t* part_keys, int n_q, int n_splits, int k_out,
+                                                  uint32_t* fold_ctr, float* __restrict__ out_s,
+                                                  int32_t* __restrict__ out_r, uint64_t* __restrict__ out_keys,
+                                                  uint64_t* lds, int* sh_last) {
+  // The lists were stored write-through (agent-scope relaxed stores: past this XCD's L2); each
+  // wave waits for its stores' acknowledgement before the barrier, so they are device-visible
+  // before the arrival. (An agent-scope fence instead writes back and invalidates the whole L2 in
+  // every workgroup: measured 62 vs 35 us per B = 1 search.)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *sh_last = __hip_atomic_fetch_add(fold_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (uint32_t)(gridDim.x - 1);
+  __syncthreads();
+  if (!*sh_last) return;
+  // every query's lists at once (read past L2 too: agent scope), then wave q walks query q
+  const int n = n_splits * k_out;
+  for (int i = threadIdx.x; i < n_q * n; i += blockDim.x)
+    lds[i] = __hip_atomic_load(part_keys + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  if (wave < n_q) walk_lists_lds(lds + wave * n, n_splits, k_out, k_out, (int64_t)wave * k_out, out_s, out_r, out_keys);
+  if (threadIdx.x == 0) __hip_atomic_store(fold_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // =============================================================================================
 // topk_small_kernel (B <= 64, bf16/f16, k <= 16): every corpus row is read once and scored
 // against at most 64 queries, so the launch is bound by the corpus stream (HBM / MALL), not by
@@ -2589,7 +2672,8 @@ template <int DT, int KCAP, int NG>
 __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
     const uint8_t* __restrict__ corpus, const float* __restrict__ qsrc, int dim, int normalize,
     const uint8_t* __restrict__ qconv, int64_t row_stride, int d_pad, int n_rows, int n_q, int n_steps,
-    int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys) {
+    int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, uint32_t* __restrict__ fold_ctr,
+    float* __restrict__ out_s, int32_t* __restrict__ out_r, uint64_t* __restrict__ out_keys) {
   static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
   constexpr int W = small::waves(NG);
   constexpr int kThreads = W * 64;
@@ -2719,9 +2803,14 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
         }
         if (lane == j) mine = best;
       }
-      if (lane < k_out) part_keys[((int64_t)q * n_splits + split) * k_out + lane] = mine;
+      if (lane < k_out)  // write-through: the fold's last workgroup may read it
+        __hip_atomic_store(part_keys + ((int64_t)q * n_splits + split) * k_out + lane, mine, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (fold_ctr)  // B <= kFoldMaxQ: the last workgroup merges the splits (no merge launch)
+    fold_last_arrival(part_keys, n_q, n_splits, k_out, fold_ctr, out_s, out_r, out_keys, lists,
+                      reinterpret_cast<int*>(lists + n_splits * k_out));
 }
 
 // topk_small_f32_kernel (fp32 exact mode, B <= 4, k <= 16): the small-batch stream for the
@@ -2742,7 +2831,9 @@ constexpr int kMaxQ = 4;
 template <int KCAP, int NQ>
 __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qconv, int64_t row_stride, int n_rows, int n_q,
-    int n_lines, int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys) {
+    int n_lines, int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
+    uint32_t* __restrict__ fold_ctr, float* __restrict__ out_s, int32_t* __restrict__ out_r,
+    uint64_t* __restrict__ out_keys) {
   constexpr int W = smallf32::kWaves;
   __shared__ __attribute__((aligned(16))) float qs[NQ * 1024];  // d_pad <= 1024
   __shared__ uint64_t wl[NQ][W][KCAP];
@@ -2864,8 +2955,16 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
         }
         if (lane == j) mine = best;
       }
-      if (lane < k_out) part_keys[((int64_t)q * n_splits + split) * k_out + lane] = mine;
+      if (lane < k_out)  // write-through: the fold's last workgroup may read it
+        __hip_atomic_store(part_keys + ((int64_t)q * n_splits + split) * k_out + lane, mine, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  if (fold_ctr) {  // the last workgroup merges the splits (no merge launch)
+    extern __shared__ __attribute__((aligned(16))) unsigned char fold_smem[];
+    uint64_t* fl = reinterpret_cast<uint64_t*>(fold_smem);
+    fold_last_arrival(part_keys, n_q, n_splits, k_out, fold_ctr, out_s, out_r, out_keys, fl,
+                      reinterpret_cast<int*>(fl + n_splits * k_out));
   }
 }
 
@@ -2902,43 +3001,7 @@ __global__ __launch_bounds__(256) void merge_block_kernel(const uint64_t* __rest
   }
   __syncthreads();
   if (wave != 0) return;
-  // one wave walks the heads (lane l owns lists l + 64 u): no barrier per output
-  constexpr int kH = 8;  // n_lists <= 512
-  int ptr[kH];
-  uint64_t head[kH];
-#pragma unroll
-  for (int u = 0; u < kH; ++u) {
-    const int l = lane + 64 * u;
-    ptr[u] = 0;
-    head[u] = (l < n_lists && k_in > 0) ? kb[l * k_in] : 0;
-  }
-  uint64_t mine = 0;  // lane j % 64 keeps the j-th winner; flushed in windows of 64 outputs
-  for (int j = 0; j < k; ++j) {
-    uint64_t m = head[0];
-#pragma unroll
-    for (int u = 1; u < kH; ++u) m = max_u64(m, head[u]);
-    const uint64_t best = wave_max_u64(m);
-    if (best != 0 && m == best) {
-#pragma unroll
-      for (int u = 0; u < kH; ++u) {
-        if (head[u] == best) {
-          const int l = lane + 64 * u;
-          ++ptr[u];
-          head[u] = ptr[u] < k_in ? kb[l * k_in + ptr[u]] : 0;
-        }
-      }
-    }
-    if (lane == (j & 63)) mine = best;
-    if ((j & 63) == 63 || j == k - 1) {  // flush a full (or the last) window of 64 outputs
-      const int j0 = j & ~63;
-      if (j0 + lane <= j) {
-        const int64_t o = (int64_t)q * k + j0 + lane;
-        if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
-        if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
-        if (keys_out) keys_out[o] = mine;
-      }
-    }
-  }
+  walk_lists_lds(kb, n_lists, k_in, k, (int64_t)q * k, scores, rows, keys_out);
 }
 
 // Cluster-probe seed (ahr_index_probe_seed): per query, the exact scores of the rows of its
@@ -3140,7 +3203,7 @@ struct ahr_index {
   uint8_t* qbuf_kb = nullptr;
   int64_t q_cap = 0;  // rows in qbuf (multiple of kRowPad)
   uint64_t* part = nullptr;
-  int64_t part_cap = 0;  // uint64 elements
+  int64_t part_cap = 0;  // uint64 elements (+ 8 more: the small kernels' fold counter, fold_ctr())
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
   int64_t sample_cap = 0;   // floats
   uint8_t* cand = nullptr;  // query-resident kernel: candidate groups (counts, row bases, scores)
@@ -3157,6 +3220,7 @@ struct ahr_index {
   std::vector<hipEvent_t> prof_events;
   int prof_max_calls = 0;
   int prof_calls = 0;
+  uint32_t* fold_ctr() const { return reinterpret_cast<uint32_t*>(part + part_cap); }
 };
 
 namespace {
@@ -3387,9 +3451,10 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
     ix->part = nullptr;
     ix->part_cap = 0;
-    if (hipMalloc(&ix->part, p_need * sizeof(uint64_t)) != hipSuccess)
+    if (hipMalloc(&ix->part, (p_need + 8) * sizeof(uint64_t)) != hipSuccess)
       return fail(AHR_ENOMEM, "partial top-k workspace allocation failed");
     ix->part_cap = p_need;
+    AHR_HIP(hipMemsetAsync(ix->part + p_need, 0, 8 * sizeof(uint64_t), s));  // fold counter
   }
   const int64_t s_need = (int64_t)B * (kGroupMax + 1);
   if (s_need > ix->sample_cap) {
@@ -3520,27 +3585,38 @@ void launch_lane_k(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, 
     launch_lane<DT, 16, NB, BJ, WR, WQ, STAGES, MINB>(ix, p, n_rows, B, k, row_base, thr, flags, s);
 }
 
+// fold != nullptr: the small kernels merge the splits themselves (B <= kFoldMaxQ, fold_ok())
+struct FoldOut {
+  uint32_t* ctr;
+  float* scores;
+  int32_t* rows;
+  uint64_t* keys;
+};
+
 template <int DT, int KCAP, int NG>
 void launch_small(const ahr_index* ix, const SearchPlan& p, const float* q, int normalize_q, int B, int k,
-                  uint32_t row_base, hipStream_t s) {
+                  uint32_t row_base, const FoldOut* fold, hipStream_t s) {
   constexpr auto kern = &topk_small_kernel<DT, KCAP, NG>;
-  const int lds = small::lds_bytes(ix->row_stride, KCAP, NG);
+  int lds = small::lds_bytes(ix->row_stride, KCAP, NG);
+  if (fold) lds = std::max(lds, B * p.n_splits * k * 8 + 16);
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::waves(NG) * 64), lds, s, ix->rows, q, ix->dim,
                      normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, (int)ix->count, B,
-                     (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part);
+                     (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part,
+                     fold ? fold->ctr : nullptr, fold ? fold->scores : nullptr, fold ? fold->rows : nullptr,
+                     fold ? fold->keys : nullptr);
 }
 
 template <int DT, int NG>
 void launch_small_k(const ahr_index* ix, const SearchPlan& p, const float* q, int normalize_q, int B, int k,
-                    uint32_t row_base, hipStream_t s) {
+                    uint32_t row_base, const FoldOut* fold, hipStream_t s) {
   if (k <= 8)
-    launch_small<DT, 8, NG>(ix, p, q, normalize_q, B, k, row_base, s);
+    launch_small<DT, 8, NG>(ix, p, q, normalize_q, B, k, row_base, fold, s);
   else if (k <= 12)
-    launch_small<DT, 12, NG>(ix, p, q, normalize_q, B, k, row_base, s);
+    launch_small<DT, 12, NG>(ix, p, q, normalize_q, B, k, row_base, fold, s);
   else
-    launch_small<DT, 16, NG>(ix, p, q, normalize_q, B, k, row_base, s);
+    launch_small<DT, 16, NG>(ix, p, q, normalize_q, B, k, row_base, fold, s);
 }
 
 // queries converted inside topk_small_kernel (convert_row_fast's shape) instead of by the convert kernel
@@ -3549,30 +3625,38 @@ inline bool small_fuses_convert(const ahr_index* ix) {
 }
 
 template <int KCAP>
-void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, hipStream_t s) {
+void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const FoldOut* fold,
+                        hipStream_t s) {
   const int n_lines = (int)(ix->row_stride / 128);
+  const size_t lds = fold ? (size_t)B * p.n_splits * k * 8 + 16 : 0;
+  uint32_t* fc = fold ? fold->ctr : nullptr;
+  float* fs = fold ? fold->scores : nullptr;
+  int32_t* fr = fold ? fold->rows : nullptr;
+  uint64_t* fk = fold ? fold->keys : nullptr;
   if (B == 1)
-    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 1>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), 0, s,
-                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part);
+    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 1>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), lds, s,
+                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part,
+                       fc, fs, fr, fk);
   else
-    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 4>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), 0, s,
-                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part);
+    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 4>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), lds, s,
+                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part,
+                       fc, fs, fr, fk);
 }
 
 template <int DT>
 void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const float* q,
-                   int normalize_q, hipStream_t s) {
+                   int normalize_q, const FoldOut* fold, hipStream_t s) {
   const float* thr = nullptr;
   prof_mark(ix, 1, s);
   if constexpr (DT == DT_F32) {
     if (p.kernel == KERNEL_SMALL) {
       prof_mark(ix, 2, s);
       if (k <= 8)
-        launch_small_f32_k<8>(ix, p, B, k, row_base, s);
+        launch_small_f32_k<8>(ix, p, B, k, row_base, fold, s);
       else if (k <= 12)
-        launch_small_f32_k<12>(ix, p, B, k, row_base, s);
+        launch_small_f32_k<12>(ix, p, B, k, row_base, fold, s);
       else
-        launch_small_f32_k<16>(ix, p, B, k, row_base, s);
+        launch_small_f32_k<16>(ix, p, B, k, row_base, fold, s);
       return;
     }
   } else {
@@ -3580,9 +3664,9 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       prof_mark(ix, 2, s);
       const float* qs = small_fuses_convert(ix) ? q : nullptr;
       switch (small::groups(B)) {
-        case 1: launch_small_k<DT, 1>(ix, p, qs, normalize_q, B, k, row_base, s); break;
-        case 2: launch_small_k<DT, 2>(ix, p, qs, normalize_q, B, k, row_base, s); break;
-        default: launch_small_k<DT, 4>(ix, p, qs, normalize_q, B, k, row_base, s); break;
+        case 1: launch_small_k<DT, 1>(ix, p, qs, normalize_q, B, k, row_base, fold, s); break;
+        case 2: launch_small_k<DT, 2>(ix, p, qs, normalize_q, B, k, row_base, fold, s); break;
+        default: launch_small_k<DT, 4>(ix, p, qs, normalize_q, B, k, row_base, fold, s); break;
       }
       return;
     }
@@ -3791,18 +3875,24 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->qbuf,
                        ix->row_stride, (int64_t)0, (int64_t)B, n_kb, ix->qbuf_kb);
   }
+  // single searches (the drop-in's search() and environment resets): the small kernels merge the
+  // splits in their last workgroup, no merge launch
+  const bool fold = ix->count > 0 && p.kernel == KERNEL_SMALL && B <= kFoldMaxQ &&
+                    (int64_t)B * p.n_splits * k * 8 + 16 <= kFoldMaxLds && p.n_splits <= 512 &&
+                    !(ix->debug_flags & kFlagNoFold);
+  const FoldOut fo{ix->fold_ctr(), scores, rows, keys};
   if (ix->count > 0) {
     switch (ix->dtype) {
-      case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, s); break;
-      case AHR_F16: launch_search<DT_F16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, s); break;
-      default: launch_search<DT_F32>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, s); break;
+      case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, fold ? &fo : nullptr, s); break;
+      case AHR_F16: launch_search<DT_F16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, fold ? &fo : nullptr, s); break;
+      default: launch_search<DT_F32>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, fold ? &fo : nullptr, s); break;
     }
   } else {
     prof_mark(ix, 1, s);
     prof_mark(ix, 2, s);
   }
   prof_mark(ix, 3, s);
-  {
+  if (!fold) {
     // qkv: one list per (split, dimension half); t256 / kb256: one per (split, row half)
     const int lists = (cand_plan ? 2 : 1) *
                       p.n_splits;
@@ -4030,7 +4120,7 @@ int ahr_index_set_seed(ahr_index* ix, const float* thr) {
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
-                             kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst);
+                             kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold);
   return AHR_OK;
 }
 

@@ -1,0 +1,107 @@
+"""Small-batch fold: at B <= 4 the small kernels' last-arriving workgroup merges the per-split lists
+(no merge launch). Results must equal the merge-launch path (flag 1 << 22) bit for bit, for every
+storage type, ties across splits, k > n, ragged splits, back-to-back calls (the arrival counter
+resets itself), the keyed query and two workspaces on two streams.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dense_ref as dr
+
+pytestmark = pytest.mark.gpu
+
+NO_FOLD = 1 << 22
+
+
+def _clustered(rng, n, d, n_centers=64, noise=0.35):
+    c = dr.normalize_rows(rng.standard_normal((n_centers, d)).astype(np.float32))
+    lab = rng.integers(0, n_centers, n)
+    return dr.normalize_rows(c[lab] + noise * rng.standard_normal((n, d)).astype(np.float32) / np.sqrt(d))
+
+
+def _pair(ix, Q, k, **kw):
+    ix.set_debug_flags(0)
+    a = [t.cpu().numpy() for t in ix.query(Q, k, **kw)]
+    ix.set_debug_flags(NO_FOLD)
+    b = [t.cpu().numpy() for t in ix.query(Q, k, **kw)]
+    ix.set_debug_flags(0)
+    return a, b
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16", "f32"])
+@pytest.mark.parametrize("n,d,B,k", [
+    (90000, 768, 1, 10), (40001, 768, 4, 16), (33000, 384, 3, 5), (300, 768, 2, 1), (5, 256, 1, 10),
+    (1000, 100, 4, 12), (257, 1024, 1, 16)])
+def test_fold_equals_merge_launch(cuda, dtype, n, d, B, k):
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(70 + n + d + B + k)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    assert ix.plan(B, k)["kernel"] == "small"
+    a, b = _pair(ix, Q, k)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0], b[0])
+    kk = min(k, n)
+    if kk < k:
+        assert (a[1][:, kk:] == -1).all() and np.isneginf(a[0][:, kk:]).all()
+    ix.close()
+
+
+def test_fold_ties_repeats_keys(cuda):
+    """Duplicated rows tie across splits (lower row first); 50 calls back to back with changing
+    B and k reuse the counter; the keyed query folds as well."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(5)
+    base = _clustered(rng, 3000, 768)
+    C = np.concatenate([base] * 10)  # row i ties with i + 3000 j
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    Qs = [_clustered(rng, 1 + (i % 4), 768) for i in range(50)]
+    ks = [1 + (i * 7) % 16 for i in range(50)]
+    got = [[t.cpu().numpy() for t in ix.query(q, k)] for q, k in zip(Qs, ks)]
+    keys = ix.query_keys(Qs[3], 10, row_base=1234).cpu().numpy()
+    ix.set_debug_flags(NO_FOLD)
+    ref = [[t.cpu().numpy() for t in ix.query(q, k)] for q, k in zip(Qs, ks)]
+    keys_ref = ix.query_keys(Qs[3], 10, row_base=1234).cpu().numpy()
+    ix.close()
+    for (gs, gr), (rs, rr) in zip(got, ref):
+        np.testing.assert_array_equal(gr, rr)
+        np.testing.assert_array_equal(gs, rs)
+    np.testing.assert_array_equal(keys, keys_ref)
+    # ties resolve to the lowest row: every returned row of a query's duplicate group is the first
+    r = got[0][1]
+    assert (np.diff(got[0][0], axis=1) <= 0).all()
+    for row in r:
+        for j in range(1, len(row)):
+            if row[j] >= 0 and row[j - 1] >= 0 and row[j] % 3000 == row[j - 1] % 3000:
+                assert row[j] > row[j - 1]
+
+
+def test_fold_two_streams(cuda):
+    """Two workspaces (two arrival counters) on two streams, interleaved single-query batches."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(11)
+    C = _clustered(rng, 60000, 768)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    Qs = [torch.from_numpy(_clustered(rng, 1 + i % 4, 768)).to(cuda) for i in range(16)]
+    serial = [[t.cpu().numpy() for t in ix.query(q, 10)] for q in Qs]
+    for i in range(2):
+        ix.set_workspace(i)
+        ix.reserve(4, 16)
+    streams = [torch.cuda.current_stream(cuda), torch.cuda.Stream(device=cuda)]
+    streams[1].wait_stream(streams[0])
+    outs = []
+    for i, q in enumerate(Qs):
+        ix.set_workspace(i % 2)
+        with torch.cuda.stream(streams[i % 2]):
+            outs.append(ix.query(q, 10))
+    torch.cuda.synchronize()
+    ix.set_workspace(0)
+    for (s, r), (es, er) in zip(outs, serial):
+        np.testing.assert_array_equal(r.cpu().numpy(), er)
+        np.testing.assert_array_equal(s.cpu().numpy(), es)
+    ix.close()
