@@ -312,7 +312,10 @@ class DenseIndex:
         8 = 128x128 tile kernel (cooperative), 32 = 128x128 lane-local kernel at any batch,
         64 = 256x128 lane kernel, 256 = group maxima only (garbage), 2048 = plan without the
         query-resident kernel, 4096 = the query-resident kernel wherever it applies, 32768 = the
-        256x256 16x16x32 kernel (bf16/f16, k <= 16), 65536 = the small-batch kernel up to B = 64."""
+        256x256 16x16x32 kernel (bf16/f16, k <= 16), 65536 = the small-batch kernel up to B = 64,
+        1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
+        1 << 20 / 1 << 21 = k-blocked kernels read every tile from tile 0 / the split's first
+        tile (garbage)."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
     _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256", "kb128")

@@ -129,9 +129,11 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
  * 4096 = the query-resident kernel wherever it applies, 32768 = the 256x256 16x16x32 kernel,
  * 65536 = the small-batch streaming kernel up to B = 64, 131072 = the k-blocked 256x256 kernel
  * wherever it applies, 262144 = never the k-blocked kernels, 524288 = the k-blocked 256x128 kernel
- * (two workgroups per CU) wherever it applies. Garbage results (cost splits):
+ * (two workgroups per CU) wherever it applies, 4194304 = small batches merge through a merge
+ * launch instead of the last-workgroup fold. Garbage results (cost splits):
  * 2 = skip the top-k epilogue, 256 = lane epilogue stops after the group maxima, 512 = tile
- * kernel (cooperative) loads operands for its first tile only. */
+ * kernel (cooperative) loads operands for its first tile only, 1048576 / 2097152 = the k-blocked
+ * kernels read every tile's operands from tile 0 / from their split's first tile. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
