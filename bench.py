@@ -79,6 +79,8 @@ def parse_args(argv=None):
     ap.add_argument("--probe-seeds", action="store_true",
                     help="seed the fused kernels from a coarse-cluster probe (DenseIndex.build_clusters, built "
                          "untimed with the index) instead of the sampled pre-pass; the probe runs inside every step")
+    ap.add_argument("--probe-clusters", type=int, default=0,
+                    help="with --probe-seeds: number of k-means clusters (0: rows / 22)")
     ap.add_argument("--debug-flags", type=int, default=0,
                     help="ablation/kernel-selection switches (DenseIndex.set_debug_flags); 0 in production")
     return ap.parse_args(argv)
@@ -301,7 +303,7 @@ def run(args) -> None:
     clusters = None
     if args.probe_seeds:  # index build, like the corpus upsert: outside the timed region
         t_cl = time.perf_counter()
-        clusters = local.build_clusters()
+        clusters = local.build_clusters(args.probe_clusters or None)
         torch.cuda.synchronize()
         clusters["build_s"] = round(time.perf_counter() - t_cl, 2)
     salt = rank if shard == "queries" else 0
