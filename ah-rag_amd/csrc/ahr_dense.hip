@@ -2691,11 +2691,18 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   const int b_end = (int)((int64_t)(split + 1) * n_blocks / n_splits);
   // the wave's work is a sequence of items (16-row block, 8 k-steps); two register sets keep the
   // next item's loads in flight under the current item's MFMAs, across block boundaries
+  // Every load is unconditional (steps past the row clamp to its last step; a finished wave
+  // re-reads its current item, an L2 hit) so that every path through the loop issues the same
+  // loads: with a conditional load the compiler's waitcnt placement must assume the younger item
+  // may not be in flight and waits vmcnt(0) before each MFMA, i.e. for the NEXT item's loads too,
+  // which serialises the stream on one memory latency per item.
   auto load_item = [&](u32x4 (&A)[small::kKC], int blk, int s0) __attribute__((always_inline)) {
-    const uint8_t* arow = corpus + (int64_t)(blk * 16 + fr) * row_stride + fq * 16 + s0 * 64;
+    const uint8_t* arow = corpus + (int64_t)(blk * 16 + fr) * row_stride + fq * 16;
 #pragma unroll
-    for (int j = 0; j < small::kKC; ++j)
-      if (s0 + j < n_steps) A[j] = *reinterpret_cast<const u32x4*>(arow + j * 64);
+    for (int j = 0; j < small::kKC; ++j) {
+      const int st = s0 + j < n_steps ? s0 + j : n_steps - 1;
+      A[j] = *reinterpret_cast<const u32x4*>(arow + st * 64);
+    }
   };
   u32x4 A0[small::kKC], A1[small::kKC];
   int cb = b_begin + wave, cs = 0;
@@ -2739,14 +2746,20 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
       ns = 0;
       nb += W;
     }
-    if (nb < b_end) load_item(N, nb, ns);
+    {
+      const bool more = nb < b_end;
+      load_item(N, more ? nb : cb, more ? ns : cs);
+    }
 #pragma unroll
-    for (int j = 0; j < small::kKC; ++j)
-      if (cs + j < n_steps) {
+    for (int j = 0; j < small::kKC; ++j) {
+      // steps past the row: a zero operand (mask, not a branch) against a valid query step
+      const uint32_t m = cs + j < n_steps ? 0xFFFFFFFFu : 0u;
+      const int st = cs + j < n_steps ? cs + j : n_steps - 1;
+      const u32x4 a = {C[j][0] & m, C[j][1] & m, C[j][2] & m, C[j][3] & m};
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
-          mfma16(C[j], *reinterpret_cast<const u32x4*>(qrow + 16 * g * pitch + (cs + j) * 64), acc[g], DT);
-      }
+      for (int g = 0; g < NG; ++g)
+        mfma16(a, *reinterpret_cast<const u32x4*>(qrow + 16 * g * pitch + st * 64), acc[g], DT);
+    }
     if (ns == 0) {
       const int r0 = cb * 16 + 4 * fq;
 #pragma unroll
@@ -2878,7 +2891,10 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
       nl = 0;
       ni += W;
     }
-    if (ni < i_end) load_line(N, ni, nl);
+    {  // unconditional (a finished wave re-reads its current line): see topk_small_kernel
+      const bool more = ni < i_end;
+      load_line(N, more ? ni : ci, more ? nl : cl);
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {  // 4 groups of 8 per line
       const f32x4 lo = __builtin_bit_cast(f32x4, C[2 * g]);
