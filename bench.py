@@ -81,6 +81,8 @@ def parse_args(argv=None):
                          "untimed with the index) instead of the sampled pre-pass; the probe runs inside every step")
     ap.add_argument("--probe-clusters", type=int, default=0,
                     help="with --probe-seeds: number of k-means clusters (0: rows / 22)")
+    ap.add_argument("--sample-rows", type=int, default=-1,
+                    help="threshold pre-pass sample rows (DenseIndex.set_sample_rows; -1 = automatic)")
     ap.add_argument("--debug-flags", type=int, default=0,
                     help="ablation/kernel-selection switches (DenseIndex.set_debug_flags); 0 in production")
     return ap.parse_args(argv)
@@ -300,6 +302,8 @@ def run(args) -> None:
             local.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
     if args.debug_flags:
         local.set_debug_flags(args.debug_flags)
+    if args.sample_rows >= 0:
+        local.set_sample_rows(args.sample_rows)
     clusters = None
     if args.probe_seeds:  # index build, like the corpus upsert: outside the timed region
         t_cl = time.perf_counter()
