@@ -4116,7 +4116,8 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
   if (!ix) return fail(AHR_EINVAL, "null index");
   if (B < 0 || k <= 0 || P <= 0 || min_rows <= 0) return fail(AHR_EINVAL, "B >= 0, k, P, min_rows > 0 required");
   if (ix->dtype == AHR_F32) return fail(AHR_EUNSUP, "cluster probe seeds: bf16 / f16 indexes");
-  if (ix->dim > kProbeMaxDim || k > kProbeMaxRows) return fail(AHR_EUNSUP, "dim <= 1024 and k <= 256");
+  if (ix->dim > kProbeMaxDim || k > kProbeMaxRows || P > 64)
+    return fail(AHR_EUNSUP, "dim <= 1024, k <= 256 and P <= 64 (one lane per offered cluster)");
   if (B == 0) return AHR_OK;
   if (!q || !cluster_keys || !list_off || !list_rows || !thr) return fail(AHR_EINVAL, "null buffer");
   DeviceGuard dg(ix->device);

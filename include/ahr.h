@@ -111,7 +111,8 @@ int ahr_index_set_sample_rows(ahr_index* ix, int rows);
  * such knob); it is how a coarse-cluster probe seeds the exact search. */
 int ahr_index_set_seed(ahr_index* ix, const float* thr);
 
-/* Cluster-probe seeds for ahr_index_set_seed (bf16 / f16 indexes, dim <= 1024): per query b, the
+/* Cluster-probe seeds for ahr_index_set_seed (bf16 / f16 indexes, dim <= 1024, P <= 64, k <= 256,
+ * at most 256 rows per query): per query b, the
  * rows of clusters key_row(cluster_keys[b][0..P)) (the packed keys of a top-P search over the
  * cluster centroids; 0 = none), taken from the CSR list_rows[list_off[c] .. list_off[c+1]) in
  * order until min_rows rows, scored exactly in fp32 against the fp32 query (normalised if
