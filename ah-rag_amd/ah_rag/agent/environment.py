@@ -8,8 +8,9 @@ Same constructor, actions, observation and info dicts. The differences are where
     GPU);
   * the node/edge counts every observation reports (reference :136-139, an O(N) networkx walk per
     step) are computed once per graph version;
-  * expand_to_lca (reference :243-299, which rebuilds the belongs_to subgraph on every call) walks
-    the cached belongs_to CSR mirror on the host: ancestor sets here are a handful of nodes.
+  * expand_to_lca (reference :243-299, which rebuilds the belongs_to subgraph on every call) runs
+    as ahr_graph_lca over the device CSR (visited set in LDS), and queries whose ancestor sets
+    exceed that kernel's capacity as ahr_graph_lca_large (visited set in global memory).
 """
 from __future__ import annotations
 
@@ -340,10 +341,18 @@ def lca_batch(hg: HierarchicalGraph, inputs: Sequence[Sequence[str]]) -> List[Li
             idx[b, :len(ids)] = dg.node_indices(ids)
     out, cnt = dg.lca(torch.from_numpy(idx))
     out_h, cnt_h = out.cpu().numpy(), cnt.cpu().numpy()
-    if (cnt_h < 0).any():
-        raise RuntimeError("expand_to_lca: an ancestor set exceeds the device kernel's capacity "
-                           "(4096 nodes, 1024 per level; include/ahr.h ahr_graph_lca)")
-    return [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] for b in range(len(inputs))]
+    res = [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] if cnt_h[b] >= 0 else None for b in range(len(inputs))]
+    over = np.nonzero(cnt_h < 0)[0]
+    if len(over):
+        # ancestor sets beyond the LDS kernel's capacity (4096 visited nodes, 1024 per level):
+        # the global-memory form of the same walk answers those queries (ahr_graph_lca_large)
+        out2, cnt2 = dg.lca_large(torch.from_numpy(idx[over]))
+        out2_h, cnt2_h = out2.cpu().numpy(), cnt2.cpu().numpy()
+        for j, b in enumerate(over):
+            if cnt2_h[j] < 0:
+                raise RuntimeError("ahr_graph_lca_large reported an overflow with max_out = n_nodes")
+            res[b] = [dg.ids[i] for i in out2_h[j, :cnt2_h[j]]]
+    return res
 
 
 def expand_batch(hg: HierarchicalGraph, action: str, inputs: Sequence[Sequence[str]], limit: int = 10

@@ -6,10 +6,11 @@ Reference seams this module replaces (Yaron9/AH-RAG):
     src/ah_rag/aggregate/semantic_aggregator.py:47,71-74;
   * the Chroma collection that stores the embeddings, hierarchical_graph.py:605-611 / :660 / :714.
 
-The encoder stays a thin PyTorch call (north star: "not re-implemented"). When
-sentence-transformers or its weights are unavailable (this image has neither), HashEncoder
-gives deterministic, L2-normalised stand-in vectors so the pipeline still runs end to end; it is
-labelled as such wherever it is used.
+The encoder stays a thin PyTorch call (north star: "not re-implemented"). sentence-transformers
+is the default, as in the reference; this image has neither the package nor weights, so a run
+here must choose another encoder explicitly (AHR_ENCODER=hash: deterministic, L2-normalised
+stand-in vectors; AHR_ENCODER=torch: the model's architecture on the GPU). Nothing falls back
+silently.
 
 DenseIndex is the device half: fp32 vectors go in, the index keeps them row-major in HBM as
 bf16 / f16 / f32 and answers batched top-k queries through libahr_hip.so. Nothing here falls
@@ -66,27 +67,45 @@ class HashEncoder:
         return out[0] if single else out
 
 
-def load_encoder(model_name: str = DEFAULT_MODEL, dim: Optional[int] = None):
-    """SentenceTransformer(model_name) when importable and cached, else HashEncoder.
+class EncoderUnavailableError(RuntimeError):
+    """The requested sentence encoder cannot be loaded (and no stand-in was asked for)."""
 
-    AHR_ENCODER=hash forces the stand-in (benchmarks use synthetic vectors anyway);
-    AHR_ENCODER=torch runs the model's architecture as a batched bf16 PyTorch forward on the GPU
-    (ah_rag.encoder.TorchEncoder: a local checkpoint directory if `model_name` is one, else seeded
-    random weights).
+
+ENCODER_MODES = ("", "sentence-transformers", "hash", "torch")
+
+
+def load_encoder(model_name: str = DEFAULT_MODEL, dim: Optional[int] = None):
+    """The query / corpus encoder, chosen by AHR_ENCODER:
+
+      unset or "sentence-transformers": SentenceTransformer(model_name), as the reference does
+          (hierarchical_graph.py:8 imports it at module load, :655 / :709-711 construct it). If the
+          package or the model cannot be loaded this raises EncoderUnavailableError — it never
+          silently degrades to stand-in vectors (a broken model load would otherwise turn search()
+          into hash-random retrieval with no signal);
+      "hash": HashEncoder, the deterministic stand-in (tests and synthetic benchmarks);
+      "torch": the model's architecture as a batched bf16 PyTorch forward on the GPU
+          (ah_rag.encoder.TorchEncoder: a local checkpoint directory if `model_name` is one, else
+          seeded random weights for a known architecture).
     """
     mode = os.environ.get("AHR_ENCODER", "").lower()
+    if mode not in ENCODER_MODES:
+        raise ValueError(f"AHR_ENCODER={mode!r}: expected one of {', '.join(repr(m) for m in ENCODER_MODES)}")
     if mode == "torch":
         from .encoder import torch_encoder
         return torch_encoder(model_name)
-    if mode != "hash":
-        try:
-            from sentence_transformers import SentenceTransformer  # type: ignore
-
-            device = "cuda" if torch.cuda.is_available() else "cpu"
-            return SentenceTransformer(model_name, device=device)
-        except Exception:
-            pass
-    return HashEncoder(model_name, dim)
+    if mode == "hash":
+        return HashEncoder(model_name, dim)
+    try:
+        from sentence_transformers import SentenceTransformer  # type: ignore
+    except ImportError as e:
+        raise EncoderUnavailableError(
+            "sentence-transformers is not installed; set AHR_ENCODER=torch (GPU forward of the model's "
+            "architecture) or AHR_ENCODER=hash (deterministic stand-in vectors) to choose another encoder") from e
+    device = "cuda" if torch.cuda.is_available() else "cpu"
+    try:
+        return SentenceTransformer(model_name, device=device)
+    except Exception as e:
+        raise EncoderUnavailableError(f"SentenceTransformer({model_name!r}) failed to load: {e}") from e
 
 
 # ----------------------------------------------------------------------------------------------

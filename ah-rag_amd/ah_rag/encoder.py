@@ -10,10 +10,12 @@ Transformer -> Pooling(mean) -> Normalize).
 
 Weights. Neither sentence-transformers nor any checkpoint is present in this image or on the GPU
 box (no network). So:
-  * if `model_name` is a local directory holding a Hugging Face BERT checkpoint (config.json +
-    weights, tokenizer.json), that checkpoint and its tokenizer are loaded (local files only);
-  * otherwise the model is built from the architecture table below with seeded random weights
-    and a deterministic hash tokenizer (words -> ids by sha1). The forward pass is the real one
+  * if `model_name` is a local directory holding a Hugging Face checkpoint (config.json +
+    weights, tokenizer.json), that checkpoint and its tokenizer are loaded through AutoModel
+    (local files only; BERT for MiniLM, MPNet for all-mpnet-base-v2);
+  * otherwise, for a model name in the architecture table below, a BERT of that size is built
+    with seeded random weights and a deterministic hash tokenizer (words -> ids by sha1); any
+    other name raises. The forward pass is the real one
     (same layers, widths, sequence lengths, so the same GPU work and the same throughput); the
     vectors are not the pretrained model's and are labelled as such (`pretrained = False`).
 The reference's own CPU path cannot run here either, so encoder outputs are parity
@@ -88,23 +90,29 @@ class TorchEncoder:
 
     def __init__(self, model_name: str = "all-MiniLM-L6-v2", device: Optional[Union[str, torch.device]] = None,
                  dtype: torch.dtype = torch.bfloat16, seed: int = 20251003) -> None:
-        from transformers import BertConfig, BertModel
+        from transformers import AutoConfig, AutoModel, BertConfig, BertModel
         if not torch.cuda.is_available():
             raise RuntimeError("TorchEncoder runs the encoder forward on a ROCm GPU")
         self.model_name = model_name
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.dtype = dtype
         local = os.path.isdir(model_name) and os.path.exists(os.path.join(model_name, "config.json"))
-        if local:  # a real checkpoint on local disk (never fetched)
-            self.model = BertModel.from_pretrained(model_name, local_files_only=True, add_pooling_layer=False,
-                                                   attn_implementation="sdpa")
-            self.max_seq_length = min(512, int(self.model.config.max_position_embeddings))
+        if local:  # a real checkpoint on local disk (never fetched), whatever its architecture
+            cfg = AutoConfig.from_pretrained(model_name, local_files_only=True)
+            extra = {"add_pooling_layer": False} if cfg.model_type in ("bert", "mpnet", "roberta",
+                                                                        "xlm-roberta") else {}
+            self.model = AutoModel.from_pretrained(model_name, local_files_only=True, attn_implementation="sdpa",
+                                                   **extra)
+            self.max_seq_length = min(512, int(getattr(self.model.config, "max_position_embeddings", 512)))
             tok_json = os.path.join(model_name, "tokenizer.json")
             self.tokenizer = _HFTokenizer(tok_json, self.max_seq_length) if os.path.exists(tok_json) else \
                 HashTokenizer(self.model.config.vocab_size, self.max_seq_length)
             self.pretrained = True
         else:
-            arch = dict(ARCHS.get(model_name, ARCHS["all-MiniLM-L6-v2"]))
+            if model_name not in ARCHS:
+                raise ValueError(f"TorchEncoder: {model_name!r} is neither a local checkpoint directory nor a "
+                                 f"known architecture ({', '.join(sorted(ARCHS))})")
+            arch = dict(ARCHS[model_name])
             self.max_seq_length = arch.pop("max_seq_length")
             cfg = BertConfig(max_position_embeddings=512, attn_implementation="sdpa", **arch)
             gen_state = torch.random.get_rng_state()

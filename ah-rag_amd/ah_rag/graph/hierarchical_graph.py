@@ -24,6 +24,7 @@ from __future__ import annotations
 import copy
 import datetime
 import hashlib
+import itertools
 import json
 import os
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -44,6 +45,10 @@ META_FILE = os.path.join(GRAPH_DIR, "meta.json")
 
 VECTORS_FILE = "ahr_vectors.npy"
 ROWS_FILE = "ahr_rows.json"
+
+# Process-wide version numbers of resident indexes: a cache keyed on one can never match a later
+# index (an id() can be reused once the old object is gone, and a per-object counter restarts).
+_INDEX_VERSIONS = itertools.count(1)
 
 
 def _sha(text: str) -> str:
@@ -137,7 +142,7 @@ class ResidentIndex:
         self.slot = {nid: i for i, nid in enumerate(self.ids)}
         self.stamp = store.stamp()
         self.full_loads += 1
-        self.version += 1
+        self.version = next(_INDEX_VERSIONS)
 
     def _alloc(self, dim: int, capacity: int) -> None:
         if self.index is not None:
@@ -172,7 +177,7 @@ class ResidentIndex:
                 self.metas.append(dict(metas[i]))
         self.rows_upserted += len(old_i) + len(new_i)
         self.stamp = store_stamp(self.path)
-        self.version += 1
+        self.version = next(_INDEX_VERSIONS)
 
     def close(self) -> None:
         if self.index is not None:
@@ -601,6 +606,7 @@ class HierarchicalGraph:
             if reset:
                 resident.close()
                 self._indexes.pop(os.path.abspath(db_path))
+                self._engines.pop(os.path.abspath(db_path), None)
             else:
                 resident.apply(todo, vectors, metas)
         new_meta = dict(prev)
@@ -636,7 +642,7 @@ class HierarchicalGraph:
         graph = self.device_graph()
         key = os.path.abspath(db_path)
         res = self.resident_index(key)
-        stamp = (id(res), res.version, id(graph))
+        stamp = (res.version, graph.serial)
         hit = self._engines.get(key)
         if hit is None or hit[0] != stamp:
             self._engines[key] = (stamp, SearchEngine(res.index, res.ids, res.metas, graph))

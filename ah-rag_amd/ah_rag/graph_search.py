@@ -19,6 +19,7 @@ the environment's limit/break rules see the same neighbour sequence (SURVEY §8a
 from __future__ import annotations
 
 import functools
+import itertools
 import json
 import math
 from dataclasses import dataclass
@@ -36,6 +37,7 @@ EDGE_TYPES = ("belongs_to", "related_to", "participates_in")
 ADJ_SPECS = (("belongs_to", "out"), ("belongs_to", "in"), ("related_to", "out"),
              ("related_to", "in"), ("participates_in", "out"), ("participates_in", "in"))
 ACTIONS = {"parents": 0, "children": 1, "related": 2}
+_GRAPH_SERIALS = itertools.count(1)  # process-wide: caches key on it instead of id()
 
 SEARCH_DEFAULTS = {  # hierarchical_graph.py:37-47
     "alpha": 0.6, "beta": 0.2, "gamma": 0.1, "delta": 0.1,
@@ -84,6 +86,7 @@ class DeviceGraph:
 
     def __init__(self, G: nx.DiGraph, device: Optional[torch.device] = None) -> None:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.serial = next(_GRAPH_SERIALS)
         self.ids: List[str] = list(G.nodes)
         self.index: Dict[str, int] = {nid: i for i, nid in enumerate(self.ids)}
         n = len(self.ids)
@@ -191,6 +194,35 @@ class DeviceGraph:
             nat.check(nat.lib().ahr_graph_lca(self._h, nat.ptr(x), B, n_in, int(max_out), nat.ptr(out), nat.ptr(cnt),
                                               nat.stream_ptr(stream)), "ahr_graph_lca")
         return out, cnt
+
+    def lca_large(self, inputs: torch.Tensor, stream: Optional[torch.cuda.Stream] = None
+                  ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """ahr_graph_lca_large: the same result as lca() without its per-query capacity (the
+        visited set lives in a global-memory workspace of 5 * n_nodes int32 per query), for the
+        queries lca() reported as over capacity. Chunked so the workspace stays <= 256 MiB."""
+        B, n_in = inputs.shape
+        dev = self.device
+        n = max(self.n_nodes, 1)
+        chunk = max(1, min(B, (256 << 20) // (20 * n)))
+        outs, cnts = [], []
+        x_all = inputs.to(device=dev, dtype=torch.int32).contiguous()
+        for b0 in range(0, B, chunk):
+            x = x_all[b0:b0 + chunk].contiguous()
+            nb = x.shape[0]
+            need = nat.ctypes.c_int64()
+            nat.check(nat.lib().ahr_graph_lca_workspace(self._h, nb, nat.ctypes.byref(need)),
+                      "ahr_graph_lca_workspace")
+            ws = torch.empty((max(need.value // 4, 1),), dtype=torch.int32, device=dev)
+            out = torch.empty((nb, n), dtype=torch.int32, device=dev)
+            cnt = torch.empty((nb,), dtype=torch.int32, device=dev)
+            _on_stream(stream, dev, x, ws, out, cnt)
+            with torch.cuda.device(dev):
+                nat.check(nat.lib().ahr_graph_lca_large(self._h, nat.ptr(x), nb, n_in, n, nat.ptr(out), nat.ptr(cnt),
+                                                        nat.ptr(ws), need.value, nat.stream_ptr(stream)),
+                          "ahr_graph_lca_large")
+            outs.append(out)
+            cnts.append(cnt)
+        return torch.cat(outs), torch.cat(cnts)
 
     def expand(self, action: str, inputs: torch.Tensor, limit: int = 10,
                stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -51,10 +51,16 @@ class SyntheticCorpus:
         self.centroids = _normalize(torch.randn(spec.n_centroids, spec.dim, generator=g)).to(self.device)
         self.topics = torch.randint(0, spec.n_centroids, (spec.n_entities,), generator=g)
 
-    def entity_chunks(self, chunk: int = 100_000) -> Iterator[Tuple[int, torch.Tensor]]:
+    def entity_chunks(self, chunk: int = 100_000, lo: int = 0, hi: Optional[int] = None
+                      ) -> Iterator[Tuple[int, torch.Tensor]]:
+        """(start, rows) chunks of the entity rows; chunks entirely outside [lo, hi) are skipped
+        without being generated (each chunk has its own seed, so any subset is reproducible)."""
         s = self.spec
+        hi = s.n_entities if hi is None else hi
         for start in range(0, s.n_entities, chunk):
             n = min(chunk, s.n_entities - start)
+            if start + n <= lo or start >= hi:
+                continue
             g = torch.Generator(device=self.device).manual_seed(s.seed + 1 + start // chunk)
             eps = torch.randn(n, s.dim, generator=g, device=self.device) / np.sqrt(s.dim)
             t = self.topics[start:start + n].to(self.device)
@@ -75,21 +81,34 @@ class SyntheticCorpus:
             out[s.n_entities:] = _normalize(sums[:s.n_summaries] + 1e-6 * self.centroids[:s.n_summaries])
         return out
 
+    def rows_at(self, idx: torch.Tensor) -> torch.Tensor:
+        """rows()[idx] without materialising the corpus: the chunks holding idx are regenerated
+        one at a time (a sharded rank never holds the other ranks' rows)."""
+        s = self.spec
+        idx = idx.to(torch.int64).cpu()
+        if s.n_summaries and bool((idx >= s.n_entities).any()):
+            return self.rows()[idx.to(self.device)]
+        out = torch.empty(len(idx), s.dim, dtype=torch.float32, device=self.device)
+        for start, x in self.entity_chunks():
+            m = (idx >= start) & (idx < start + x.shape[0])
+            if bool(m.any()):
+                out[m.nonzero().squeeze(1).to(self.device)] = x[(idx[m] - start).to(self.device)]
+        return out
+
     def queries(self, batch: int, rows: Optional[torch.Tensor] = None, salt: int = 0
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
-        """(queries fp32 [batch, dim], source_row int64 [batch] or -1 for fresh draws)."""
+        """(queries fp32 [batch, dim], source_row int64 [batch] or -1 for fresh draws). Without
+        `rows`, the source rows are regenerated chunk by chunk (rows_at)."""
         s = self.spec
         g = torch.Generator(device="cpu").manual_seed(s.seed + 7919 * (salt + 1))
         half = batch // 2
-        if rows is None:
-            rows = self.rows()
-        n_rows = rows.shape[0]  # == spec.n_rows unless the caller truncated the corpus
+        n_rows = rows.shape[0] if rows is not None else s.n_rows  # rows may be a truncated corpus
         src = torch.randint(0, n_rows, (half,), generator=g)
         t = torch.randint(0, s.n_centroids, (batch - half,), generator=g)
         eps = torch.randn(batch, s.dim, generator=g) / np.sqrt(s.dim)
         eps = eps.to(self.device)
-        base = torch.cat([rows[src.to(rows.device)].to(self.device),
-                          self.centroids[t.to(self.device)]])
+        src_rows = rows[src.to(rows.device)].to(self.device) if rows is not None else self.rows_at(src)
+        base = torch.cat([src_rows, self.centroids[t.to(self.device)]])
         scale = torch.cat([torch.full((half, 1), 0.2), torch.full((batch - half, 1), s.noise)]).to(self.device)
         q = _normalize(base + scale * eps)
         source = torch.cat([src, torch.full((batch - half,), -1, dtype=torch.int64)])
@@ -134,3 +153,18 @@ def build_hotpot_graph(corpus: SyntheticCorpus, rng: Optional[np.random.Generato
         for i in rng.choice(pool, k, replace=False):
             hg.add_participation(eids[int(i)], hid)
     return hg, eids + sids
+
+
+def install_vectors(hg, ids, vectors: np.ndarray, db_path: str, model: str = "synthetic") -> None:
+    """What build_vector_index (hierarchical_graph.py:602-673) stores for the nodes `ids`, with
+    given corpus vectors instead of an encoder's (no weights offline): the on-disk vector store and
+    G.graph["vector_index"] with its sha1 indexed_meta."""
+    from .graph.hierarchical_graph import VectorStore
+    store = VectorStore(db_path)
+    store.clear()
+    metas = [hg._embedding_text(n)[1] for n in ids]
+    store.upsert(ids, np.asarray(vectors, np.float32), metas)
+    store.save(model)
+    hg.G.graph["vector_index"] = {"db_path": db_path, "model": model, "indexed_nodes": len(ids),
+                                  "indexed_meta": {n: hg._index_key(hg.G.nodes[n]) for n in ids}}
+    hg.G.graph["dirty"] = False

@@ -2594,7 +2594,7 @@ __device__ __forceinline__ void walk_lists_lds(const uint64_t* kb, int n_lists, 
 // merges the n_splits lists of each query (walk_lists_lds) and writes the outputs, so a single
 // search() is one launch instead of search + merge_block_kernel (the merge launch and its gap
 // were ~7 of ~35 us at B = 1). The counter is reset by that workgroup for the next launch on the
-// workspace. lds: n_q * n_splits * k_out keys (<= kFoldMaxLds), then the arrival flag (no static LDS: the small
+// workspace. lds: n_q * n_splits * k_out keys, then the arrival flag (<= kFoldMaxLds in all; no static LDS: the small
 // kernel opts in to 160 KiB of dynamic LDS, which leaves none). Nothing waits: no workgroup depends on another's
 // progress, so there is no residency requirement.
 constexpr int kFoldMaxQ = 4;
@@ -2615,7 +2615,13 @@ __device__ __forceinline__ void fold_last_arrival(const uint64_t* part_keys, int
     *sh_last = __hip_atomic_fetch_add(fold_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                (uint32_t)(gridDim.x - 1);
   __syncthreads();
+  // sh_last sits past every query's lists (the fill below must not overwrite it while a lagging
+  // wave has yet to test it)
   if (!*sh_last) return;
+  // Only the last workgroup acquires: one agent-scope acquire fence (cache invalidate) per search,
+  // not the release write-back in every workgroup that cost 62 vs 35 us; the lists themselves were
+  // written through with agent-scope stores whose acknowledgements were waited for above.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // every query's lists at once (read past L2 too: agent scope), then wave q walks query q
   const int n = n_splits * k_out;
   for (int i = threadIdx.x; i < n_q * n; i += blockDim.x)
@@ -2823,7 +2829,7 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   }
   if (fold_ctr)  // B <= kFoldMaxQ: the last workgroup merges the splits (no merge launch)
     fold_last_arrival(part_keys, n_q, n_splits, k_out, fold_ctr, out_s, out_r, out_keys, lists,
-                      reinterpret_cast<int*>(lists + n_splits * k_out));
+                      reinterpret_cast<int*>(lists + (int64_t)n_q * n_splits * k_out));
 }
 
 // topk_small_f32_kernel (fp32 exact mode, B <= 4, k <= 16): the small-batch stream for the
@@ -2980,7 +2986,7 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
     extern __shared__ __attribute__((aligned(16))) unsigned char fold_smem[];
     uint64_t* fl = reinterpret_cast<uint64_t*>(fold_smem);
     fold_last_arrival(part_keys, n_q, n_splits, k_out, fold_ctr, out_s, out_r, out_keys, fl,
-                      reinterpret_cast<int*>(fl + n_splits * k_out));
+                      reinterpret_cast<int*>(fl + (int64_t)n_q * n_splits * k_out));
   }
 }
 
@@ -4136,6 +4142,14 @@ int ahr_index_set_seed(ahr_index* ix, const float* thr) {
 
 int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
+  // The cost-split switches give wrong results by design; only the ablation build
+  // (__graft_entry__.build_ablation, -DAHR_ABLATION) accepts them, the shipped library refuses.
+  constexpr int kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
+                                    kFlagTileFirst;
+#ifndef AHR_ABLATION
+  if (flags & kWrongResultFlags)
+    return fail(AHR_EUNSUP, "result-corrupting ablation flags need the AHR_ABLATION build");
+#endif
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
                              kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold);
   return AHR_OK;

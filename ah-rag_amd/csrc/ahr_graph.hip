@@ -330,6 +330,98 @@ __global__ __launch_bounds__(256) void lca_kernel(DevGraph g, const int32_t* __r
   if (tid == 0) out_count[q] = overflow ? -1 : min(nout, max_out);
 }
 
+// The same walk without capacity limits, for the queries lca_kernel reports as over capacity (a
+// topic with more than 1024 members, an L2 summary above 4096 descendants). Per query a direct-
+// indexed workspace in global memory of 5 * n_nodes int32: last input per node, inputs per node,
+// the visited list (each node once, so the lowest-member scan only looks at reached nodes) and two
+// BFS frontiers, each bounded by n_nodes because a node enters an input's frontier once. The
+// kernel clears its own workspace, so nothing has to be initialised between calls. The per-node
+// words are written with device-scope atomics and read back with agent-scope atomic loads (L2),
+// never through the vector L1.
+__global__ __launch_bounds__(256) void lca_global_kernel(DevGraph g, const int32_t* __restrict__ inputs, int n_in,
+                                                         int max_out, int32_t* __restrict__ out,
+                                                         int32_t* __restrict__ out_count, int32_t* __restrict__ ws) {
+  __shared__ int32_t nvis;
+  __shared__ int32_t nfront[2];
+  __shared__ int32_t nout;
+  __shared__ int32_t overflow;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t n = g.n_nodes;
+  int32_t* last = ws + (int64_t)q * 5 * n;
+  int32_t* cnt = last + n;
+  int32_t* vis = cnt + n;
+  int32_t* front[2] = {vis + n, vis + 2 * n};
+  for (int64_t i = tid; i < n; i += 256) {
+    __hip_atomic_store(&last[i], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cnt[i], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) {
+    nvis = 0;
+    nout = 0;
+    overflow = 0;
+  }
+  __syncthreads();
+  auto claim = [&](int32_t v, int i) -> bool {
+    const int32_t prev = atomicExch(&last[v], i);
+    if (prev == i) return false;
+    if (prev == -1) vis[atomicAdd(&nvis, 1)] = v;
+    atomicAdd(&cnt[v], 1);
+    return true;
+  };
+  auto count_of = [&](int32_t v) -> int32_t {
+    return __hip_atomic_load(&cnt[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  int n_valid = 0;
+  for (int i = 0; i < n_in; ++i) {
+    const int32_t src = inputs[(int64_t)q * n_in + i];
+    if (src < 0 || src >= n) continue;  // uniform
+    ++n_valid;
+    if (tid == 0) {
+      nfront[0] = 0;
+      nfront[1] = 0;
+      if (claim(src, i)) {
+        front[0][0] = src;
+        nfront[0] = 1;
+      }
+    }
+    __syncthreads();
+    int cur = 0;
+    while (nfront[cur] > 0) {
+      const int nf = nfront[cur];
+      for (int j = tid; j < nf; j += 256) {
+        const int32_t v = front[cur][j];
+        for (int64_t e = g.off[ADJ_BT_IN][v]; e < g.off[ADJ_BT_IN][v + 1]; ++e) {
+          const int32_t u = g.tgt[ADJ_BT_IN][e];
+          if (claim(u, i)) front[cur ^ 1][atomicAdd(&nfront[cur ^ 1], 1)] = u;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) nfront[cur] = 0;
+      __syncthreads();
+      cur ^= 1;
+    }
+    __syncthreads();
+  }
+  const int nv = nvis;
+  for (int s = tid; s < nv; s += 256) {
+    const int32_t v = vis[s];
+    if (n_valid == 0 || count_of(v) != n_valid) continue;
+    bool lowest = true;
+    for (int64_t e = g.off[ADJ_BT_OUT][v]; e < g.off[ADJ_BT_OUT][v + 1] && lowest; ++e)
+      if (count_of(g.tgt[ADJ_BT_OUT][e]) == n_valid) lowest = false;
+    if (lowest) {
+      const int slot = atomicAdd(&nout, 1);
+      if (slot < max_out)
+        out[(int64_t)q * max_out + slot] = v;
+      else
+        atomicOr(&overflow, 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) out_count[q] = overflow ? -1 : min(nout, max_out);
+}
+
 }  // namespace graph
 }  // namespace ahr
 
@@ -455,6 +547,31 @@ int ahr_graph_lca(ahr_graph* g, const int32_t* inputs, int B, int n_in, int max_
   DeviceGuardG dg(g->device);
   hipLaunchKernelGGL(lca_kernel, dim3((unsigned)B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), g->dg,
                      inputs, n_in, max_out, out, out_count);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_graph_lca_workspace(const ahr_graph* g, int B, int64_t* bytes) {
+  if (!g || !bytes) return fail(AHR_EINVAL, "null graph or output");
+  if (B < 0) return fail(AHR_EINVAL, "negative size");
+  *bytes = (int64_t)B * 5 * g->n_nodes * (int64_t)sizeof(int32_t);
+  return AHR_OK;
+}
+
+int ahr_graph_lca_large(ahr_graph* g, const int32_t* inputs, int B, int n_in, int max_out, int32_t* out,
+                        int32_t* out_count, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!g) return fail(AHR_EINVAL, "null graph");
+  if (B < 0 || n_in < 0 || max_out < 0) return fail(AHR_EINVAL, "negative size");
+  if (B == 0) return AHR_OK;
+  if ((n_in > 0 && !inputs) || !out_count || (max_out > 0 && !out)) return fail(AHR_EINVAL, "null buffer");
+  int64_t need = 0;
+  (void)ahr_graph_lca_workspace(g, B, &need);
+  if (need > 0 && (!workspace || workspace_bytes < need))
+    return fail(AHR_EINVAL, "workspace smaller than ahr_graph_lca_workspace(B)");
+  if (reinterpret_cast<uintptr_t>(workspace) % 4 != 0) return fail(AHR_EINVAL, "workspace not 4-byte aligned");
+  DeviceGuardG dg(g->device);
+  hipLaunchKernelGGL(lca_global_kernel, dim3((unsigned)B), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     g->dg, inputs, n_in, max_out, out, out_count, static_cast<int32_t*>(workspace));
   AHR_HIP(hipGetLastError());
   return AHR_OK;
 }

@@ -73,6 +73,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-n1-ref", action="store_true", help="rows mode: skip the unsharded rank-0 timing")
     ap.add_argument("--no-f32-line", action="store_true",
                     help="N=1 hotpot90k: skip the exact-mode (fp32 index) line beside the bf16 headline")
+    ap.add_argument("--no-batch-sweep", action="store_true",
+                    help="N=1 hotpot90k: skip the B = 1 and B = 64 lines beside the B = 1024 headline")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (one stream + index workspace each)")
     ap.add_argument("--recall-queries", type=int, default=256)
@@ -103,12 +105,12 @@ def numpy_topk(corpus: np.ndarray, queries: np.ndarray, k: int, row_base: int = 
     return np.take_along_axis(s, idx, axis=1), idx.astype(np.int64) + row_base
 
 
-def numpy_topk_chunked(rows: torch.Tensor, queries: np.ndarray, k: int, chunk: int = 250_000):
-    """Exact fp32 top-k over a device-resident corpus too large for one host copy."""
+def numpy_topk_chunked(chunks, queries: np.ndarray, k: int):
+    """Exact fp32 top-k over a corpus given as (start, device rows) chunks, never held whole."""
     best_s = np.full((len(queries), k), -np.inf, np.float32)
     best_r = np.full((len(queries), k), -1, np.int64)
-    for s0 in range(0, rows.shape[0], chunk):
-        cs, cr = numpy_topk(rows[s0:s0 + chunk].cpu().numpy(), queries, k, row_base=s0)
+    for s0, x in chunks:
+        cs, cr = numpy_topk(x.cpu().numpy(), queries, k, row_base=s0)
         alls, allr = np.concatenate([best_s, cs], 1), np.concatenate([best_r, cr], 1)
         order = np.lexsort((allr, -alls), axis=1)[:, :k]
         best_s, best_r = np.take_along_axis(alls, order, 1), np.take_along_axis(allr, order, 1)
@@ -264,6 +266,39 @@ def read_traffic(kernel: str, workload: str, batch: int):
     return None
 
 
+def roofline(plan: dict, dtype: str, B: int, n_rows: int, d: int, k: int, tile_ms: float, workload: str) -> dict:
+    """Roofline of the dominant (tile) kernel: algorithmic flops = 2*B*N*d and bytes = N*d*s +
+    B*d*s + B*k*8 per launch over its event-timed average launch; bound = the
+    lower of the two ceilings by arithmetic intensity against the ridge."""
+    flops = 2.0 * B * n_rows * d
+    achieved_tf = flops / (tile_ms * 1e-3) / 1e12
+    peak = MFMA_PEAK_TFLOPS[dtype]
+    elem = 4 if dtype == "f32" else 2
+    alg_bytes = n_rows * d * elem + B * d * elem + B * k * 8
+    kname = KERNEL_NAMES.get(plan["kernel"], "topk_tile_kernel")
+    if plan["kernel"] == "small":
+        kname = "topk_small_f32_kernel" if dtype == "f32" else "topk_small_kernel"
+    # arithmetic intensity 2*B*N*d / (N*d*elem) against the ridge (peak flops / HBM bytes):
+    # small batches are bound by the corpus stream
+    hbm_bound = flops / alg_bytes < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    hbm_gbs = alg_bytes / (tile_ms * 1e-3) / 1e9
+    return {
+        "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} "
+                  f"Q.N^T + top-k, {plan['kernel']})",
+        "bound": "hbm" if hbm_bound else "mfma",
+        "achieved": round(hbm_gbs if hbm_bound else achieved_tf, 2),
+        "peak": HBM_PEAK_GBS if hbm_bound else peak,
+        "unit": "GB/s" if hbm_bound else "TFLOP/s",
+        "frac": round(hbm_gbs / HBM_PEAK_GBS if hbm_bound else achieved_tf / peak, 4),
+        "traffic": read_traffic(kname, workload, B),
+        "algorithmic_flops_per_launch": flops,
+        "algorithmic_bytes_per_launch": alg_bytes,
+        "hbm_equiv_GBs": round(hbm_gbs, 1),
+        "mfma_TFLOPs": round(achieved_tf, 2),
+        "avg_launch_ms": round(tile_ms, 5),
+    }
+
+
 def run(args) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -286,20 +321,31 @@ def run(args) -> None:
     dtype = args.dtype or ("bf16" if workload == "hotpot90k" else "f16")
     B, k = args.batch, args.k
     corpus = SyntheticCorpus(spec, dev)
-    rows = corpus.rows()
-    N, d = rows.shape
+    N, d = spec.n_rows, spec.dim
+    # The 5M corpus (no summary rows) is generated chunk by chunk (each chunk has its own seed)
+    # and never held whole: a row-sharded rank generates and stores only its own shard. The 90k
+    # corpus needs all entity rows for its summary rows, and is small.
+    rows = corpus.rows() if spec.n_summaries else None
+
+    def corpus_chunks(lo: int = 0, hi: int = N):
+        if rows is not None:
+            for s0 in range(lo, hi, 1_000_000):
+                yield s0, rows[s0:min(hi, s0 + 1_000_000)]
+        else:
+            yield from corpus.entity_chunks(lo=lo, hi=hi)
+
     sharded = shard == "rows" and world > 1
     if sharded:
         index = ShardedDenseIndex(d, N, dtype=dtype, device=dev)
         lo, hi = index.lo, index.hi
-        for s0 in range(0, N, 1_000_000):
-            index.upsert_global(s0, rows[s0:min(N, s0 + 1_000_000)])
+        for s0, x in corpus_chunks(lo, hi):
+            index.upsert_global(s0, x)
         local = index.local
     else:
         lo, hi = 0, N
         index = local = DenseIndex(d, N, dtype=dtype, device=dev)
-        for s0 in range(0, N, 1_000_000):
-            local.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
+        for s0, x in corpus_chunks():
+            local.upsert(x, start=s0)
     if args.debug_flags:
         local.set_debug_flags(args.debug_flags)
     if args.sample_rows >= 0:
@@ -383,8 +429,8 @@ def run(args) -> None:
     n1_qps = None
     if sharded and rank == 0 and not args.no_n1_ref:
         full = DenseIndex(d, N, dtype=dtype, device=dev)
-        for s0 in range(0, N, 1_000_000):
-            full.upsert(rows[s0:min(N, s0 + 1_000_000)], start=s0)
+        for s0, x in corpus_chunks():
+            full.upsert(x, start=s0)
         full.reserve(B, k)
         for _ in range(max(2, args.warmup)):
             full.query(q, k)
@@ -402,29 +448,17 @@ def run(args) -> None:
         # ---- recall@10 against exact fp32 ground truth of the fp32 source vectors (untimed)
         nq = min(args.recall_queries if N <= 200_000 else min(args.recall_queries, 128), B)
         qh = q[:nq].cpu().numpy()
-        if N <= 200_000:
+        if rows is not None:
             _, exact = numpy_topk(rows.cpu().numpy(), qh, k)
         else:
-            _, exact = numpy_topk_chunked(rows, qh, k)
+            _, exact = numpy_topk_chunked(corpus_chunks(), qh, k)
         got_global = got_rows[:nq] if sharded else got_rows[:nq] + lo
         rec = recall_at_k(got_global, exact)
 
         calls = max(1, prof["calls"])
         tile_ms = prof["ms_sum"]["tile_topk"] / calls
         n_local = hi - lo
-        flops = 2.0 * B * n_local * d
-        achieved_tf = flops / (tile_ms * 1e-3) / 1e12
-        peak = MFMA_PEAK_TFLOPS[dtype]
-        elem = 4 if dtype == "f32" else 2
-        alg_bytes = n_local * d * elem + B * d * elem + B * k * 8
         plan = local.plan(B, k)
-        kname = KERNEL_NAMES.get(plan["kernel"], "topk_tile_kernel")
-        if plan["kernel"] == "small":
-            kname = "topk_small_f32_kernel" if dtype == "f32" else "topk_small_kernel"
-        # arithmetic intensity 2*B*N*d / (N*d*elem) against the ridge (peak flops / HBM bytes):
-        # small batches are bound by the corpus stream
-        hbm_bound = flops / alg_bytes < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-        hbm_gbs = alg_bytes / (tile_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -452,20 +486,7 @@ def run(args) -> None:
                                    if clusters else "sampled pre-pass"),
             },
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
-            "roofline": {
-                "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} "
-                          f"Q.N^T + top-k, {plan['kernel']})",
-                "bound": "hbm" if hbm_bound else "mfma",
-                "achieved": round(hbm_gbs if hbm_bound else achieved_tf, 2),
-                "peak": HBM_PEAK_GBS if hbm_bound else peak,
-                "unit": "GB/s" if hbm_bound else "TFLOP/s",
-                "frac": round(hbm_gbs / HBM_PEAK_GBS if hbm_bound else achieved_tf / peak, 4),
-                "traffic": read_traffic(kname, workload, B),
-                "algorithmic_flops_per_launch": flops,
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "hbm_equiv_GBs": round(hbm_gbs, 1),
-                "avg_launch_ms": round(tile_ms, 5),
-            },
+            "roofline": roofline(plan, dtype, B, n_local, d, k, tile_ms, workload),
             "cpu_baseline": None,
         }
         if sharded:
@@ -489,10 +510,32 @@ def run(args) -> None:
                              "unit": "TFLOP/s", "frac": round(f_tf / MFMA_PEAK_TFLOPS["f32"], 4)},
             }
             f32.close()
+        if world == 1 and workload == "hotpot90k" and not args.no_batch_sweep:
+            # BASELINE.md's C2 batch sweep beside the B = 1024 headline: B = 1 (the drop-in
+            # search() / RL reset; streaming kernel, HBM-bound) and B = 64 (tile path), same index
+            out["batch_sweep"] = []
+            for b in (1, 64):
+                qb = q[:b].contiguous()
+                b_steps = args.steps * 4
+                b_dt, b_prof, _ = time_queries(local, qb, k, b_steps, args.warmup, inflight, dev)
+                b_calls = max(1, b_prof["calls"])
+                b_plan = local.plan(b, k)
+                out["batch_sweep"].append({
+                    "batch": b, "value": round(b * b_steps / b_dt, 1), "unit": "queries/s",
+                    "ms_per_step": round(b_dt / b_steps * 1e3, 4), "steps": b_steps, "launch": b_plan,
+                    "stages_ms_per_step": {kk: round(v / b_calls, 4) for kk, v in b_prof["ms_sum"].items()},
+                    "roofline": roofline(b_plan, dtype, b, N, d, k, b_prof["ms_sum"]["tile_topk"] / b_calls,
+                                         workload)})
         if world == 1 and not args.no_cpu_baseline:
             nc = min(len(q), 1024)
-            out["cpu_baseline"] = cpu_baseline(rows.cpu().numpy(), q[:nc].cpu().numpy(), k, args.cpu_seconds,
-                                               workload)
+            if rows is not None:
+                host_rows = rows.cpu().numpy()
+            else:  # assembled chunk by chunk on the host
+                host_rows = np.empty((N, d), np.float32)
+                for s0, x in corpus_chunks():
+                    host_rows[s0:s0 + x.shape[0]] = x.cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(host_rows, q[:nc].cpu().numpy(), k, args.cpu_seconds, workload)
+            del host_rows
         print(json.dumps(out), flush=True)
     index.close()
     if world > 1:

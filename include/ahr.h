@@ -124,17 +124,18 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
                          int P, const int64_t* list_off, const int32_t* list_rows, int min_rows, float* thr,
                          void* stream);
 
-/* Ablation switches for profiling, never set in production. Correct results: 8 = always the
+/* Kernel-selection switches (A/B measurements; results stay correct): 8 = always the
  * 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile kernel at any
  * batch (k <= 16), 64 = the 256x128 lane kernel (k <= 16), 2048 = no query-resident kernel,
  * 4096 = the query-resident kernel wherever it applies, 32768 = the 256x256 16x16x32 kernel,
  * 65536 = the small-batch streaming kernel up to B = 64, 131072 = the k-blocked 256x256 kernel
  * wherever it applies, 262144 = never the k-blocked kernels, 524288 = the k-blocked 256x128 kernel
  * (two workgroups per CU) wherever it applies, 4194304 = small batches merge through a merge
- * launch instead of the last-workgroup fold. Garbage results (cost splits):
- * 2 = skip the top-k epilogue, 256 = lane epilogue stops after the group maxima, 512 = tile
- * kernel (cooperative) loads operands for its first tile only, 1048576 / 2097152 = the k-blocked
- * kernels read every tile's operands from tile 0 / from their split's first tile. */
+ * launch instead of the last-workgroup fold, 16384 = tilelane without the cross-tile prefetch.
+ * Cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
+ * only, 512 = operands of the first tile only, 1024 = loads never waited for, 1048576 / 2097152 =
+ * k-blocked tiles read from tile 0 / the split's first tile) are accepted only by the ablation
+ * build (-DAHR_ABLATION, __graft_entry__.build_ablation); the shipped library returns AHR_EUNSUP. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
@@ -257,6 +258,15 @@ int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int
  * by (level, id) and truncates (:289), and checks acyclicity once per graph version. */
 int ahr_graph_lca(ahr_graph* g, const int32_t* inputs, int B, int n_in, int max_out, int32_t* out,
                   int32_t* out_count, void* stream);
+
+/* The same computation without per-query capacity limits, for the queries ahr_graph_lca reported
+ * as over capacity (count -1 with max_out large enough): the visited set and frontiers live in a
+ * caller-owned device workspace of ahr_graph_lca_workspace(B) bytes (5 * n_nodes int32 per query,
+ * cleared by the kernel itself). out_count is -1 only when max_out is too small (max_out =
+ * n_nodes never is). Same reference semantics (environment.py:243-289). */
+int ahr_graph_lca_workspace(const ahr_graph* g, int B, int64_t* bytes);
+int ahr_graph_lca_large(ahr_graph* g, const int32_t* inputs, int B, int n_in, int max_out, int32_t* out,
+                        int32_t* out_count, void* workspace, int64_t workspace_bytes, void* stream);
 
 int ahr_graph_info(const ahr_graph* g, int64_t* n_nodes, int64_t* n_edges);
 

@@ -256,3 +256,92 @@ def isclose_dicts(a, b, tol: float = 0.0, ignore=("updated_at",)) -> bool:
             return a == b
         return a == b or (tol > 0 and math.isclose(float(a), float(b), abs_tol=tol))
     return a == b
+
+
+class GymEpisode:
+    """One AHRAGGymEnv episode restated on a networkx graph: the GraphEnvironment state (selection /
+    frontier sets, step count), its observations and the gym's action dispatch, reward and done
+    rule. Restates environment.py:118-150 (_observation), :155-241 (reset / semantic_anchor),
+    :301-355 (query_node_details, commit_selection), :393-480 (expansions via env_expand) and
+    gym_env.py:41-125 (reset, get_action_mask, _pick_top_ids, step). The dense search result is
+    given to reset() as the search() cluster (expand_rerank of the oracle's dense top-k)."""
+
+    TOP = {0: 2, 1: 2, 2: 1, 3: 3, 4: 1}
+    EXPAND = {0: "parents", 1: "children", 2: "related"}
+
+    def __init__(self, G: nx.DiGraph, max_steps: int = 6, repeat_penalty: float = 0.02) -> None:
+        self.G = G
+        self.counts = {"n_nodes": G.number_of_nodes(), "n_edges": G.number_of_edges()}
+        self.max_steps = max(1, int(max_steps))
+        self.repeat_penalty = float(repeat_penalty)
+
+    def _brief_scored(self, res: Dict[str, Any]) -> Dict[str, Any]:
+        b = node_brief(self.G, res.get("node_id"))
+        b.update({"score": res.get("score"), "semantic": res.get("semantic")})
+        return b
+
+    def _observation(self, seeds, reranked) -> Dict[str, Any]:
+        return {"selection": [self._brief_scored(x) for x in reranked],
+                "seeds": [self._brief_scored(x) for x in seeds],
+                "state": {"selection_ids": sorted(self.selection), "frontier_ids": sorted(self.frontier)[:50]},
+                "counts": dict(self.counts), "step": self.env_step}
+
+    def mask(self) -> List[int]:
+        if not (self.raw or {}).get("selection"):
+            return [0, 0, 0, 0, 0, 1]
+        return [1] * 6
+
+    def reset(self, cluster: Dict[str, Any]) -> Tuple[np.ndarray, Dict[str, Any]]:
+        self.selection, self.frontier = set(), set()
+        self.env_step = 1  # reset -> semantic_anchor
+        self.cur = 0
+        self.last_action = None
+        reranked = cluster.get("reranked", [])
+        self.frontier = {x.get("node_id") for x in reranked if x.get("node_id")}
+        self.raw = self._observation(cluster.get("seeds", []), reranked)
+        return featurize(self.raw), self.raw
+
+    def _top(self, k: int) -> List[str]:
+        return [n["node_id"] for n in (self.raw.get("selection") or [])[:k] if n.get("node_id")]
+
+    def step(self, action: int) -> Tuple[np.ndarray, float, bool, Dict[str, Any]]:
+        self.cur += 1
+        prev = self.raw
+        done = False
+        if action in self.EXPAND:
+            self.env_step += 1
+            ids = env_expand(self.G, self.EXPAND[action], self._top(self.TOP[action]), 10)
+            obs = self._observation([{"node_id": n, "semantic": 0.0} for n in ids],
+                                    [{"node_id": n, "score": 0.0, "semantic": 0.0} for n in ids])
+            self.frontier.update(ids)
+        elif action == 3:
+            self.env_step += 1
+            added = []
+            for nid in self._top(3):
+                if nid in self.G and nid not in self.selection:
+                    self.selection.add(nid)
+                    added.append(nid)
+                    self.frontier.discard(nid)
+            obs = self._observation([], [{"node_id": n, "score": 0.0, "semantic": 0.0} for n in added])
+        elif action == 4:
+            ids = self._top(1)
+            if ids:
+                self.env_step += 1
+                d = self.G.nodes[ids[0]]
+                details = {**node_brief(self.G, ids[0]), "title": d.get("title"), "name": d.get("name"),
+                           "summary_text": (d.get("summary_text") or d.get("summary") or "")[:500],
+                           "description": (d.get("description") or "")[:500],
+                           "top_words": d.get("top_words"), "members": d.get("members")}
+                obs = {"selection": [details], "seeds": [], "counts": dict(self.counts), "step": self.env_step}
+            else:
+                obs = prev
+        else:
+            done = True
+            obs = prev
+        r = 0.0 if done else step_reward(prev, obs)
+        if not done and self.last_action is not None and action == self.last_action and self.repeat_penalty > 0:
+            r -= self.repeat_penalty
+        done = done or self.cur >= self.max_steps
+        self.raw = obs
+        self.last_action = action
+        return featurize(obs), float(r), bool(done), obs

@@ -91,3 +91,11 @@ def test_torch_encoder_self_retrieval(cuda, tmp_path, monkeypatch):
         assert top["node_id"] in by_text[texts[n]], n
         assert top["semantic"] > 0.999
     json.dumps(res)  # plain JSON-able result dicts, as the reference returns
+
+
+@pytest.mark.gpu
+def test_torch_encoder_rejects_unknown_names(cuda):
+    """Unknown model names raise instead of silently becoming MiniLM with random weights."""
+    from ah_rag.encoder import TorchEncoder
+    with pytest.raises(ValueError, match="known architecture"):
+        TorchEncoder("my-org/not-a-model", cuda)

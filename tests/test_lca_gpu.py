@@ -1,7 +1,7 @@
 """Device expand_to_lca (ahr_graph_lca) against the oracle's restatement of the reference
 (oracle/search_ref.env_lca <- environment.py:243-299) on the reference's own saved graph, batched
 over many input lists: single inputs, duplicates, summaries of both levels, entity/summary mixes,
-padding; plus the capacity guard (a query beyond the kernel's LDS tables raises, never answers)."""
+padding; plus queries beyond the LDS kernel's tables, answered by the global-memory kernel."""
 import os
 
 import numpy as np
@@ -37,15 +37,51 @@ def test_lca_batch_matches_oracle(cuda):
     assert lca_batch(hg, [[]]) == [[]]
 
 
-def test_lca_capacity_guard(cuda):
-    """An ancestor set larger than the kernel's per-query table raises instead of truncating."""
+def test_lca_large_matches_lds_kernel(cuda):
+    """ahr_graph_lca_large (global-memory visited set) gives lca()'s answers on every case."""
+    import torch
+    from ah_rag.graph.hierarchical_graph import HierarchicalGraph
+    hg = HierarchicalGraph.load(os.path.join(GOLDEN, "reference_graph"))
+    dg = hg.device_graph()
+    G = hg.G
+    dag_nodes = sorted({n for u, v, a in G.edges(data=True) if a.get("edge_type") == "belongs_to" for n in (u, v)})
+    rng = np.random.default_rng(9)
+    idx = np.full((200, 5), -1, np.int32)
+    for b in range(200):
+        m = int(rng.integers(0, 6))
+        idx[b, :m] = dg.node_indices([dag_nodes[int(i)] for i in rng.integers(0, len(dag_nodes), m)])
+    o1, c1 = dg.lca(torch.from_numpy(idx))
+    o2, c2 = dg.lca_large(torch.from_numpy(idx))
+    o1, c1, o2, c2 = o1.cpu().numpy(), c1.cpu().numpy(), o2.cpu().numpy(), c2.cpu().numpy()
+    assert (c1 >= 0).all() and np.array_equal(c1, c2)
+    for b in range(200):
+        assert sorted(o1[b, :c1[b]]) == sorted(o2[b, :c2[b]])
+
+
+def test_lca_over_capacity_matches_oracle(cuda):
+    """Ancestor sets beyond the LDS kernel's tables (4096 visited nodes, 1024 per BFS level) are
+    answered by ahr_graph_lca_large, with the reference's result (it used to raise)."""
     import networkx as nx
-    from ah_rag.agent.environment import lca_batch
+    from ah_rag.agent.environment import GraphEnvironment, lca_batch
     from ah_rag.graph.hierarchical_graph import HierarchicalGraph
     hg = HierarchicalGraph()
     top = hg.add_summary(0, title="top")
-    for i in range(5000):  # 5000 members of one summary: its ancestor set exceeds 4096 nodes
-        hg.add_belongs_to(hg.add_entity(f"e{i}"), top)
-    with pytest.raises(RuntimeError, match="capacity"):
-        lca_batch(hg, [[top]])
+    mids = [hg.add_summary(1 + j, title=f"mid{j}") for j in range(3)]
+    ents = [hg.add_entity(f"e{i}") for i in range(5000)]
+    for i, e in enumerate(ents):  # 5000 members of one summary: its ancestor set exceeds 4096 nodes
+        hg.add_belongs_to(e, top)
+        if i % 2 == 0:
+            hg.add_belongs_to(e, mids[i % 3])
+    for m in mids:
+        hg.add_belongs_to(m, top)
+    G = hg.G
+    cases = [[top], [top, mids[0]], mids[:2], [mids[1]], [top, top], [ents[0], top], [mids[2], ents[4]]]
+    got = lca_batch(hg, cases)
+    for ids, g in zip(cases, got):
+        want, _ = search_ref.env_lca(G, ids, max_results=10 ** 6)
+        assert _sorted(G, g, 10 ** 6) == want, ids
+    env = GraphEnvironment(graph=hg, logging_enabled=False)
+    obs, info = env.expand_to_lca([top, mids[0]])
+    want, _ = search_ref.env_lca(G, [top, mids[0]])
+    assert [x["node_id"] for x in obs["selection"]] == want and info["lca_count"] == len(want)
     assert isinstance(hg.G, nx.DiGraph)

@@ -105,3 +105,35 @@ def test_fold_two_streams(cuda):
         np.testing.assert_array_equal(r.cpu().numpy(), er)
         np.testing.assert_array_equal(s.cpu().numpy(), es)
     ix.close()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_fold_empty_split_lists(cuda, dtype):
+    """B = 2..4 over a corpus smaller than the split count: most (query, split) lists are empty
+    (key 0), so query 1's first key is 0. The arrival flag must not live there (a fast
+    wave's LDS fill overwrote it, a lagging wave saw "not last" and the outputs were lost). 60
+    back-to-back calls per shape, every one against the oracle."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(17)
+    for n in (3, 40, 200):
+        C = _clustered(rng, n, 768)
+        ix = DenseIndex(768, n, dtype=dtype, device=cuda)
+        ix.upsert(C)
+        Cs = dr.round_to_storage(C, dtype) if dtype != "f32" else C
+        for it in range(60):
+            B = 2 + it % 3
+            k = 1 + (it * 5) % 16
+            Q = _clustered(rng, B, 768)
+            assert ix.plan(B, k)["kernel"] == "small"
+            s, r = (t.cpu().numpy() for t in ix.query(Q, k))
+            kk = min(k, n)
+            if dtype == "f32":
+                es, er = dr.topk(C, Q, k, mode="fma")
+                np.testing.assert_array_equal(r, er)
+                np.testing.assert_array_equal(s, es.astype(np.float32))
+            else:
+                es, er = dr.topk(Cs, dr.round_to_storage(Q, dtype), k, mode="f64")
+                assert np.abs(s[:, :kk] - es[:, :kk]).max() < 1e-4
+                assert (r[:, :kk] >= 0).all()
+            assert (r[:, kk:] == -1).all()
+        ix.close()

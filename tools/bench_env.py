@@ -30,20 +30,7 @@ import torch.distributed as dist  # noqa: E402
 from ah_rag.agent.gym_env import AHRAGGymEnv  # noqa: E402
 from ah_rag.agent.vec_env import VecAHRAGGymEnv  # noqa: E402
 from ah_rag.distributed import launch  # noqa: E402
-from ah_rag.graph.hierarchical_graph import HierarchicalGraph, VectorStore  # noqa: E402
-from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph  # noqa: E402
-
-
-def install_vectors(hg: HierarchicalGraph, ids, vectors: np.ndarray, db_path: str) -> None:
-    """What build_vector_index stores, with the corpus vectors instead of an encoder's."""
-    store = VectorStore(db_path)
-    store.clear()
-    metas = [hg._embedding_text(n)[1] for n in ids]
-    store.upsert(ids, vectors, metas)
-    store.save("synthetic")
-    hg.G.graph["vector_index"] = {"db_path": db_path, "model": "synthetic", "indexed_nodes": len(ids),
-                                  "indexed_meta": {n: hg._index_key(hg.G.nodes[n]) for n in ids}}
-    hg.G.graph["dirty"] = False
+from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph, install_vectors  # noqa: E402
 
 
 def random_actions(rng, masks):
