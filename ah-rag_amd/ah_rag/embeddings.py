@@ -333,11 +333,13 @@ class DenseIndex:
         query-resident kernel, 4096 = the query-resident kernel wherever it applies, 32768 = the
         256x256 16x16x32 kernel (bf16/f16, k <= 16), 65536 = the small-batch kernel up to B = 64,
         1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
+        1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 768, k <= 12),
         1 << 20 / 1 << 21 = k-blocked kernels read every tile from tile 0 / the split's first
         tile (garbage)."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
-    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256", "kb128")
+    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256", "kb128",
+                "qres256")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

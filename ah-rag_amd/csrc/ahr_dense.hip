@@ -31,6 +31,8 @@
 // query's threshold with a valid lower bound of its final k-th best score.
 #include "ahr_common.h"
 #include "ahr.h"
+#include "ahr_dense_common.h"
+#include "ahr_qres.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -40,167 +42,6 @@
 namespace ahr {
 namespace dense {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-enum { DT_F32 = AHR_F32, DT_F16 = AHR_F16, DT_BF16 = AHR_BF16 };
-
-constexpr int kThreads = 256;
-constexpr int kTileRows = 128;
-constexpr int kTileQ = 128;
-constexpr int kRowBytes = 128;  // one k-tile of one row: 8 chunks of 16 B
-constexpr int kBufBytes = (kTileRows + kTileQ) * kRowBytes;  // 32 KiB: A tile, then B tile
-constexpr int kProdCap = 8;  // candidate slots per (query, producer lane); 4 producers per query
-
-// LDS map (bytes). The candidate lists overlay the two staging buffers: they are only live
-// between the last k-tile of a corpus tile and the first k-tile of the next one.
-constexpr int kOffBuf0 = 0;
-constexpr int kOffBuf1 = kBufBytes;
-constexpr int kOffCand = 0;
-constexpr int kCandBytes = kTileQ * 4 * kProdCap * 8;   // 32 KiB
-constexpr int kOffScratch = kOffCand + kCandBytes;         // 4 waves x 64 lanes x 32 floats
-constexpr int kScratchBytes = 4 * 64 * 32 * 4;             // 32 KiB
-constexpr int kOffThrKey = 2 * kBufBytes;
-constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
-constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
-constexpr int kOffFlag = kOffCnt + kTileQ * 4 * 4;
-constexpr int kLdsBytes = kOffFlag + 16;
-static_assert(kCandBytes + kScratchBytes <= 2 * kBufBytes, "epilogue overlay must fit the staging buffers");
-static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
-
-// XOR swizzle of 16-B chunks inside a 128-B row: a ds_read_b128 lane group (rows
-// {0-3,12-15,20-27} or {4-11,16-19,28-31} of a 32-row fragment, same chunk) then covers all
-// 16 slots of a 256-B bank row (conflict-free).
-__device__ __forceinline__ int swz(int row, int chunk) {
-  return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4);
-}
-// 64-B rows (half k-tiles): a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the
-// row so the 16 rows of a ds_read_b128 lane group hit 16 distinct 16-B slots.
-__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
-
-// Sorted (descending) register list of packed keys; drops the smallest on insert.
-template <int KCAP>
-__device__ __forceinline__ void list_insert(uint64_t (&L)[KCAP], uint64_t key) {
-  if (key <= L[KCAP - 1]) return;
-#pragma unroll
-  for (int j = KCAP - 1; j > 0; --j) {
-    const uint64_t prev = L[j - 1];
-    L[j] = (prev < key) ? prev : ((L[j] < key) ? key : L[j]);
-  }
-  L[0] = (L[0] < key) ? key : L[0];
-}
-
-// Wave64 max of packed keys with DPP row shifts + row broadcasts (gfx9 family): no LDS
-// round trips, unlike __shfl_xor (ds_bpermute). Returns the max in every lane.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROW_MASK, 0xf, false);
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
-
-__device__ __forceinline__ uint64_t max_u64(uint64_t a, uint64_t b) { return a > b ? a : b; }
-
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-  x = max_u64(x, dpp_u64<0x111, 0xf>(x));  // row_shr:1
-  x = max_u64(x, dpp_u64<0x112, 0xf>(x));  // row_shr:2
-  x = max_u64(x, dpp_u64<0x114, 0xf>(x));  // row_shr:4
-  x = max_u64(x, dpp_u64<0x118, 0xf>(x));  // row_shr:8  -> lane 15 of each row: row max
-  x = max_u64(x, dpp_u64<0x142, 0xa>(x));  // row_bcast:15 -> lane 31, 63: max of row pairs
-  x = max_u64(x, dpp_u64<0x143, 0xc>(x));  // row_bcast:31 -> lane 63: wave max
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
-  const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// LDS-DMA through a buffer descriptor (MUBUF `buffer_load ... lds`). Unlike the FLAT-encoded
-// global_load_lds, LLVM does not count it as a possibly out-of-order LDS access, so the
-// fragment reads that follow keep counted lgkmcnt(N) waits. The descriptor covers one tile
-// (32-bit offsets, whatever the corpus size) and must be built from wave-uniform values.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-
-__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
-                                           0, 0);
-}
-
-// Workgroup barrier that waits for this wave's LDS traffic but leaves global_load_lds in flight
-// (__syncthreads() would emit vmcnt(0) and drain the ring).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int DT>
-__device__ __forceinline__ void mfma_step(const u32x4& a, const u32x4& b, f32x16& acc) {
-  if constexpr (DT == DT_BF16) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
-                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
-  } else if constexpr (DT == DT_F16) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
-                                                 __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
-  } else {
-    // fp32: the chunk holds k = 8g + 2m + h for m = 0..3 (storage permutation), so four
-    // k-ordered 32x32x2 steps extend one fma chain in increasing k (exact-mode contract).
-    const f32x4 af = __builtin_bit_cast(f32x4, a);
-    const f32x4 bf = __builtin_bit_cast(f32x4, b);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[m], bf[m], acc, 0, 0, 0);
-  }
-}
-
-// Runtime-indexed read of a register list without scratch: a select chain. The opaque copy
-// of j stops LLVM from folding the chain back into an indexed load (which would demote the
-// whole list to scratch memory).
-template <int KCAP>
-__device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) {
-  uint64_t v = L[0];
-#pragma unroll
-  for (int j = 1; j < KCAP; ++j) {
-    int jj = j;
-    asm volatile("" : "+s"(jj));
-    v = (jj == idx) ? L[j] : v;
-  }
-  return v;
-}
-
-enum { MODE_TOPK = 0, MODE_GROUPMAX = 1, MODE_SCORES = 2 };
-enum {
-  kFlagXcdRemap = 1,
-  kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
-  kFlagTile128 = 8,       // the 128x128 tile kernel with cooperative screening, any k
-  kFlagTileLane = 32,     // the 128x128 lane-local kernel at any batch (k <= 16)
-  kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
-  kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
-  kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
-  kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
-  kFlagNoQres = 2048,     // plan without the query-resident kernel
-  kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
-  kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
-  kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagSmallWide = 65536,  // the small-batch kernel up to B = 64 (2 or 4 query groups; measured slower)
-  kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagNoKB256 = 262144,  // plan without the k-blocked kernels
-  kFlagKB128 = 524288,    // the k-blocked 256x128 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagTileZero = 1 << 20,   // k-blocked kernels: every tile's operands read from tile 0 (L2-resident; wrong results)
-  kFlagTileFirst = 1 << 21,  // k-blocked kernels: every tile read from the split's first tile (wrong results)
-  kFlagNoFold = 1 << 22,     // small kernels: merge launch instead of the last-workgroup fold (A/B)
-};
-constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
-                             kFlagKB256 | kFlagNoKB256 | kFlagKB128;
-// every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 // MODE_TOPK : per-(query, split) top-k lists into part_keys [n_q][n_splits][k_out].
 //             thr_init (optional, [n_q]) seeds each query's threshold with a score that is a
@@ -3271,11 +3112,12 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 }
 
 // ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
+// 10 = 256-query register-resident kernel (ahr_qres.hip),
 // 3 = 128x128 lane-local tile kernel, 5 = query-resident kernel (dimension halves over wave pairs);
 // 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed), 6 = 256x256 16x16x32
 // kernel (opt-in), 7 = small-batch streaming kernel (B <= 16; <= 64 opt-in)
 enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
-       KERNEL_T256 = 6, KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_KB128 = 9 };
+       KERNEL_T256 = 6, KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_KB128 = 9, KERNEL_QRES = 10 };
 
 struct SearchPlan {
   int kernel;
@@ -3356,9 +3198,35 @@ bool kb128_ok(const ahr_index* ix, int B, int k) {
   return (ix->debug_flags & kFlagKB128) != 0;
 }
 
+// The 256-query register-resident kernel (ahr_qres.hip): bf16/f16 at d_pad = 768, k <= 12, from
+// kQresMinBatch queries on, when the threshold pre-pass runs (its admission threshold is the seed
+// until a lane's own k-th best passes it). Debug flags force it (kFlagQres) or keep it out
+// (kFlagNoQres, or any other kernel flag).
+constexpr int kQresMinBatch = 512;
+bool qres_ok(const ahr_index* ix, int B, int k) {
+  if (!qres::supported(ix->dtype, ix->d_pad * ix->elem, k) || B <= 0) return false;
+  if (ix->debug_flags & kFlagNoQres) return false;
+  if (ix->debug_flags & kFlagQres) return true;
+  if (ix->debug_flags & kKernelFlags) return false;  // another kernel explicitly requested
+  const int S = sample_rows_for(ix);
+  return B >= kQresMinBatch && S > 0 && ix->count >= 4 * (int64_t)S;
+}
+
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
+  if (!small_ok(ix, B, k) && qres_ok(ix, B, k)) {
+    // one workgroup of 8 waves per CU, 256 queries each: one wave of 256 workgroups
+    p.kernel = KERNEL_QRES;
+    p.qblocks = (int)cdiv(B, qres::kTQ);
+    p.n_row_tiles = (int)cdiv(ix->count, qres::kTR);
+    int want = std::max(1, 256 / p.qblocks);
+    want = std::min(want, std::max(1, p.n_row_tiles));
+    p.xcd_remap = want >= 8;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    return p;
+  }
   if (small_ok(ix, B, k)) {
     // one workgroup per CU, at least one 16-row block per wave
     p.kernel = KERNEL_SMALL;
@@ -3710,6 +3578,11 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const int n = (int)ix->count;
   const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
+    if (p.kernel == KERNEL_QRES) {
+      qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, n, B, row_base, ix->part, thr, p.n_splits,
+                   p.qblocks, flags, s);
+      return;
+    }
     if (p.kernel == KERNEL_KB256) {
       if (k <= 8)
         launch_kb256<DT, 8, 4>(ix, p, n, B, k, row_base, thr, flags, s);
@@ -3896,6 +3769,15 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     const int64_t chunks = (int64_t)B * n_kb * 4;
     hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->qbuf,
                        ix->row_stride, (int64_t)0, (int64_t)B, n_kb, ix->qbuf_kb);
+  }
+  if (p.kernel == KERNEL_QRES && ix->count > 0) {
+    // the register-resident kernel's B operand: a fragment-major copy of the converted queries
+    if (!ix->qbuf_kb) {
+      if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
+        return fail(AHR_ENOMEM, "query workspace allocation failed");
+      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
+    }
+    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, k, ix->qbuf_kb, ix->debug_flags, s);
   }
   // single searches (the drop-in's search() and environment resets): the small kernels merge the
   // splits in their last workgroup, no merge launch
@@ -4145,13 +4027,15 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   // The cost-split switches give wrong results by design; only the ablation build
   // (__graft_entry__.build_ablation, -DAHR_ABLATION) accepts them, the shipped library refuses.
   constexpr int kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
-                                    kFlagTileFirst;
+                                    kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead;
 #ifndef AHR_ABLATION
   if (flags & kWrongResultFlags)
     return fail(AHR_EUNSUP, "result-corrupting ablation flags need the AHR_ABLATION build");
 #endif
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
-                             kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold);
+                             kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold |
+                             kFlagNoBarrier | kFlagNoLdsRead | kFlagQresStagger | kFlagQresScreenLoop |
+                             kFlagQres16);
   return AHR_OK;
 }
 

@@ -1,0 +1,194 @@
+// Device helpers shared by the dense-search translation units of libahr_hip.so (gfx950):
+// fragment types, LDS swizzles, register top-k lists, DPP reductions, buffer LDS-DMA,
+// MFMA steps and the ablation / plan flag bits.
+#pragma once
+
+#include "ahr_common.h"
+#include "ahr.h"
+
+namespace ahr {
+namespace dense {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum { DT_F32 = AHR_F32, DT_F16 = AHR_F16, DT_BF16 = AHR_BF16 };
+
+constexpr int kThreads = 256;
+constexpr int kTileRows = 128;
+constexpr int kTileQ = 128;
+constexpr int kRowBytes = 128;  // one k-tile of one row: 8 chunks of 16 B
+constexpr int kBufBytes = (kTileRows + kTileQ) * kRowBytes;  // 32 KiB: A tile, then B tile
+constexpr int kProdCap = 8;  // candidate slots per (query, producer lane); 4 producers per query
+
+// LDS map (bytes). The candidate lists overlay the two staging buffers: they are only live
+// between the last k-tile of a corpus tile and the first k-tile of the next one.
+constexpr int kOffBuf0 = 0;
+constexpr int kOffBuf1 = kBufBytes;
+constexpr int kOffCand = 0;
+constexpr int kCandBytes = kTileQ * 4 * kProdCap * 8;   // 32 KiB
+constexpr int kOffScratch = kOffCand + kCandBytes;         // 4 waves x 64 lanes x 32 floats
+constexpr int kScratchBytes = 4 * 64 * 32 * 4;             // 32 KiB
+constexpr int kOffThrKey = 2 * kBufBytes;
+constexpr int kOffThrScore = kOffThrKey + kTileQ * 8;
+constexpr int kOffCnt = kOffThrScore + kTileQ * 4;
+constexpr int kOffFlag = kOffCnt + kTileQ * 4 * 4;
+constexpr int kLdsBytes = kOffFlag + 16;
+static_assert(kCandBytes + kScratchBytes <= 2 * kBufBytes, "epilogue overlay must fit the staging buffers");
+static_assert(kLdsBytes % 16 == 0, "LDS carve must stay 16-B aligned");
+
+// XOR swizzle of 16-B chunks inside a 128-B row: a ds_read_b128 lane group (rows
+// {0-3,12-15,20-27} or {4-11,16-19,28-31} of a 32-row fragment, same chunk) then covers all
+// 16 slots of a 256-B bank row (conflict-free).
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+// 64-B rows (half k-tiles): a 256-B bank row holds 4 rows; XOR the chunk with bits 2-3 of the
+// row so the 16 rows of a ds_read_b128 lane group hit 16 distinct 16-B slots.
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// Sorted (descending) register list of packed keys; drops the smallest on insert.
+template <int KCAP>
+__device__ __forceinline__ void list_insert(uint64_t (&L)[KCAP], uint64_t key) {
+  if (key <= L[KCAP - 1]) return;
+#pragma unroll
+  for (int j = KCAP - 1; j > 0; --j) {
+    const uint64_t prev = L[j - 1];
+    L[j] = (prev < key) ? prev : ((L[j] < key) ? key : L[j]);
+  }
+  L[0] = (L[0] < key) ? key : L[0];
+}
+
+// Wave64 max of packed keys with DPP row shifts + row broadcasts (gfx9 family): no LDS
+// round trips, unlike __shfl_xor (ds_bpermute). Returns the max in every lane.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROW_MASK, 0xf, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ uint64_t max_u64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+  x = max_u64(x, dpp_u64<0x111, 0xf>(x));  // row_shr:1
+  x = max_u64(x, dpp_u64<0x112, 0xf>(x));  // row_shr:2
+  x = max_u64(x, dpp_u64<0x114, 0xf>(x));  // row_shr:4
+  x = max_u64(x, dpp_u64<0x118, 0xf>(x));  // row_shr:8  -> lane 15 of each row: row max
+  x = max_u64(x, dpp_u64<0x142, 0xa>(x));  // row_bcast:15 -> lane 31, 63: max of row pairs
+  x = max_u64(x, dpp_u64<0x143, 0xc>(x));  // row_bcast:31 -> lane 63: wave max
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+  const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// LDS-DMA through a buffer descriptor (MUBUF `buffer_load ... lds`). Unlike the FLAT-encoded
+// global_load_lds, LLVM does not count it as a possibly out-of-order LDS access, so the
+// fragment reads that follow keep counted lgkmcnt(N) waits. The descriptor covers one tile
+// (32-bit offsets, whatever the corpus size) and must be built from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
+                                           0, 0);
+}
+
+// the same with a compile-time byte offset (the instruction's 12-bit immediate: no extra VGPR)
+template <int IMM>
+__device__ __forceinline__ void blds16_imm(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
+  static_assert(IMM >= 0 && IMM < 4096, "buffer instruction offset field");
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, IMM,
+                                           0);
+}
+
+// Workgroup barrier that waits for this wave's LDS traffic but leaves global_load_lds in flight
+// (__syncthreads() would emit vmcnt(0) and drain the ring).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int DT>
+__device__ __forceinline__ void mfma_step(const u32x4& a, const u32x4& b, f32x16& acc) {
+  if constexpr (DT == DT_BF16) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  } else if constexpr (DT == DT_F16) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                 __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
+  } else {
+    // fp32: the chunk holds k = 8g + 2m + h for m = 0..3 (storage permutation), so four
+    // k-ordered 32x32x2 steps extend one fma chain in increasing k (exact-mode contract).
+    const f32x4 af = __builtin_bit_cast(f32x4, a);
+    const f32x4 bf = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[m], bf[m], acc, 0, 0, 0);
+  }
+}
+
+// Runtime-indexed read of a register list without scratch: a select chain. The opaque copy
+// of j stops LLVM from folding the chain back into an indexed load (which would demote the
+// whole list to scratch memory).
+template <int KCAP>
+__device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) {
+  uint64_t v = L[0];
+#pragma unroll
+  for (int j = 1; j < KCAP; ++j) {
+    int jj = j;
+    asm volatile("" : "+s"(jj));
+    v = (jj == idx) ? L[j] : v;
+  }
+  return v;
+}
+
+enum { MODE_TOPK = 0, MODE_GROUPMAX = 1, MODE_SCORES = 2 };
+enum {
+  kFlagXcdRemap = 1,
+  kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
+  kFlagTile128 = 8,       // the 128x128 tile kernel with cooperative screening, any k
+  kFlagTileLane = 32,     // the 128x128 lane-local kernel at any batch (k <= 16)
+  kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
+  kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
+  kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
+  kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
+  kFlagNoQres = 2048,     // plan without the query-resident kernels (qkv and qres)
+  kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
+  kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
+  kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
+  kFlagSmallWide = 65536,  // the small-batch kernel up to B = 64 (2 or 4 query groups; measured slower)
+  kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
+  kFlagNoKB256 = 262144,  // plan without the k-blocked kernels
+  kFlagKB128 = 524288,    // the k-blocked 256x128 kernel wherever it applies (bf16/f16, k <= 16)
+  kFlagTileZero = 1 << 20,   // k-blocked kernels: every tile's operands read from tile 0 (L2-resident; wrong results)
+  kFlagTileFirst = 1 << 21,  // k-blocked kernels: every tile read from the split's first tile (wrong results)
+  kFlagNoFold = 1 << 22,     // small kernels: merge launch instead of the last-workgroup fold (A/B)
+  kFlagQres = 1 << 23,       // the 256-query register-resident kernel wherever it applies (bf16/f16, d 768, k <= 12)
+  kFlagNoBarrier = 1 << 24,  // qres kernel: no stage barriers (wrong results)
+  kFlagNoLdsRead = 1 << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
+  kFlagQresStagger = 1 << 26,     // qres kernel: waves 4-7 one stage behind waves 0-3 (A/B; same results)
+  kFlagQresScreenLoop = 1 << 27,  // qres kernel: pass-mask + select-chain screening (A/B; same results)
+  kFlagQres16 = 1 << 28,          // qres: the 16x16x32 form (k <= 10; A/B)
+};
+#ifdef AHR_ABLATION
+constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
+#else
+constexpr bool kAblation = false;
+#endif
+constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
+                             kFlagKB256 | kFlagNoKB256 | kFlagKB128 | kFlagQres;
+// every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
+
+}  // namespace dense
+}  // namespace ahr

@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0
 KERNEL_NAMES = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel",
                 "tilelane128": "topk_tilelane_kernel", "t256": "topk_t256_kernel",
                 "qkv128": "topk_qkv_kernel", "kb256": "topk_kb256_kernel",
-                "kb128": "topk_kb256_kernel"}
+                "kb128": "topk_kb256_kernel", "qres256": "topk_qres_kernel"}
 
 
 def parse_args(argv=None):

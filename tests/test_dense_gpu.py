@@ -210,7 +210,8 @@ def test_default_plans(cuda):
     from ah_rag.embeddings import DenseIndex
     ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
     ix.upsert(np.zeros((90000, 768), np.float32))
-    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
+    assert ix.plan(1024, 10)["kernel"] == "qres256"  # tests/test_qres_gpu.py
+    assert ix.plan(1024, 13)["kernel"] == "tilelane128"
     assert ix.plan(1, 16)["kernel"] == "small"
     assert ix.plan(16, 10)["kernel"] == "small"
     assert ix.plan(17, 10)["kernel"] == "tilelane128"

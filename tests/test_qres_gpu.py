@@ -1,0 +1,191 @@
+"""The 256-query register-resident kernel (csrc/ahr_qres.hip) — the default B >= 512 bf16/f16 plan at
+d = 768, k <= 12 (the C2 headline shape; reference src/ah_rag/graph/hierarchical_graph.py:714).
+
+Two forms, each chaining the MFMA steps of an existing kernel in the same k order, so scores AND
+rows must be bitwise equal to that kernel: the default 32x32x16 form to the lane-local tile kernel
+(topk_tilelane_kernel), the v_mfma_f32_16x16x32 form (flag 1 << 28, k <= 10) to the 256x256 tile
+kernel (topk_t256_kernel, itself bitwise equal to the k-blocked and small-batch kernels) — including
+ragged row and query blocks, splits with no rows, no threshold seed (every score a candidate: the
+survivor buffers' compaction path), adversarial row order, exact ties (lowest row id first) and
+row-base offsets. Against the f64 oracle the half-precision tolerance of test_dense_gpu.py applies.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dense_ref as dr
+
+pytestmark = pytest.mark.gpu
+
+QRES = 1 << 23      # plan the register-resident kernel wherever it applies
+QRES16 = 1 << 28    # ... in its 16x16x32 form
+TILELANE = 32       # the lane-local 128x128 tile kernel at any batch
+T256 = 32768        # the 256x256 16x16x32 tile kernel
+
+
+def _clustered(rng, n, d, n_centers=50, noise=0.35):
+    c = dr.normalize_rows(rng.standard_normal((n_centers, d)).astype(np.float32))
+    lab = rng.integers(0, n_centers, n)
+    x = c[lab] + noise * rng.standard_normal((n, d)).astype(np.float32) / np.sqrt(d)
+    return dr.normalize_rows(x)
+
+
+def _run(ix, Q, k, flags, kernel):
+    ix.set_debug_flags(flags)
+    assert ix.plan(len(Q), k)["kernel"] == kernel
+    out = [t.cpu().numpy() for t in ix.query(Q, k)]
+    ix.set_debug_flags(0)
+    return out
+
+
+def _check_forms(ix, Q, k):
+    """Both forms against their reference kernels, bitwise; returns the default (32x32x16) form's
+    result. The 16x16x32 form covers k <= 10 (k = 11, 12 fall back to the 32x32x16 form)."""
+    a = _run(ix, Q, k, QRES, "qres256")
+    d = _run(ix, Q, k, TILELANE, "tilelane128")
+    np.testing.assert_array_equal(a[1], d[1])
+    np.testing.assert_array_equal(a[0], d[0])
+    c = _run(ix, Q, k, QRES | QRES16, "qres256")
+    ref = _run(ix, Q, k, T256, "t256") if k <= 10 else a
+    np.testing.assert_array_equal(c[1], ref[1])
+    np.testing.assert_array_equal(c[0], ref[0])
+    return a
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n,B,k,sample", [
+    (90000, 1024, 10, 8192),  # the C2 shape
+    (40001, 512, 10, 8192),   # ragged last row block
+    (40001, 700, 1, 8192),    # ragged query block (a partly live wave, whole dead waves), k = 1
+    (40001, 1024, 12, 0),     # no seed: compaction from the first block on
+    (33000, 2048, 8, 8192),
+    (5000, 600, 10, 0),
+    (300, 512, 5, 0),         # 10 row blocks over 8 splits, queries 300.. of the second block dead
+])
+def test_qres_matches_tilelane(cuda, dtype, n, B, k, sample):
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(501 + n + B + k + sample)
+    C = _clustered(rng, n, 768)
+    Q = _clustered(rng, B, 768)
+    ix = DenseIndex(768, n, dtype=dtype, device=cuda)
+    ix.upsert(C)
+    ix.set_sample_rows(sample)
+    a = _check_forms(ix, Q, k)
+    ix.close()
+    # and against the f64 oracle on the rounded inputs (sampled queries)
+    sel = np.arange(0, B, max(1, B // 48))
+    es, _ = dr.topk(dr.round_to_storage(C, dtype), dr.round_to_storage(Q[sel], dtype), k, mode="f64")
+    kk = min(k, n)
+    assert np.abs(a[0][sel, :kk] - es[:, :kk]).max() < 1e-4
+
+
+def test_qres_default_plan(cuda):
+    from ah_rag.embeddings import DenseIndex
+    ix = DenseIndex(768, 90000, dtype="bf16", device=cuda)
+    ix.upsert(np.zeros((90000, 768), np.float32))
+    assert ix.plan(1024, 10)["kernel"] == "qres256"
+    p = ix.plan(1024, 10)
+    assert (p["qblocks"], p["n_splits"]) == (4, 64)
+    assert ix.plan(512, 12)["kernel"] == "qres256"
+    assert ix.plan(511, 10)["kernel"] == "tilelane128"
+    assert ix.plan(1024, 13)["kernel"] == "tilelane128"  # k beyond the lane buffer's reach
+    ix.set_debug_flags(2048)
+    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
+    ix.close()
+    ix = DenseIndex(768, 20000, dtype="bf16", device=cuda)  # no pre-pass below 4 x 8192 rows
+    ix.upsert(np.zeros((20000, 768), np.float32))
+    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
+    ix.close()
+    ix = DenseIndex(384, 90000, dtype="bf16", device=cuda)  # not the resident dimension
+    ix.upsert(np.zeros((90000, 384), np.float32))
+    assert ix.plan(1024, 10)["kernel"] != "qres256"
+    ix.close()
+    ix = DenseIndex(768, 90000, dtype="f32", device=cuda)  # exact mode keeps the fp32 tile kernel
+    ix.upsert(np.zeros((90000, 768), np.float32))
+    assert ix.plan(1024, 10)["kernel"] == "tilelane128"
+    ix.close()
+
+
+@pytest.mark.parametrize("sample,k", [(8192, 10), (0, 10), (0, 12)])
+def test_qres_adversarial_order(cuda, sample, k):
+    """Rows sorted so that every row beats the ones before it for query 0 (each row a new record of
+    that lane: the buffer fills and compacts again and again) and the seed is drawn from the worst
+    rows; other queries see the same rows in clustered order."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(61 + sample)
+    C = _clustered(rng, 40000, 768)
+    Q = _clustered(rng, 1024, 768)
+    C = C[np.argsort(C @ Q[0])]
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ix.set_sample_rows(sample)
+    _check_forms(ix, Q, k)
+    ix.close()
+
+
+def test_qres_ties_order_by_row(cuda):
+    """bf16 duplicate rows score identically: the lowest row ids win, across blocks and splits."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(19)
+    base = _clustered(rng, 300, 768)
+    C = np.concatenate([base] * 120)  # 36000 rows, each vector 120 times
+    pick = rng.integers(0, 300, 600)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    for flags, k in ((QRES, 10), (QRES, 12), (QRES | QRES16, 10)):
+        s, r = _run(ix, base[pick], k, flags, "qres256")
+        np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(k)[None, :])
+        assert (s == s[:, :1]).all()
+    ix.close()
+
+
+def test_qres_sharded_keys(cuda):
+    """row_base offsets and the key merge through the register-resident plan == one unsharded query
+    (the C4 shape in miniature)."""
+    from ah_rag.embeddings import DenseIndex, merge_topk_keys
+    rng = np.random.default_rng(23)
+    C = _clustered(rng, 120000, 768)
+    Q = _clustered(rng, 1024, 768)
+    full = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    full.upsert(C)
+    assert full.plan(len(Q), 10)["kernel"] == "qres256"
+    fs, fr = [t.cpu().numpy() for t in full.query(Q, 10)]
+    full.close()
+    bounds = [0, 40001, 80000, 120000]
+    lists = []
+    for g in range(3):
+        ix = DenseIndex(768, bounds[g + 1] - bounds[g], dtype="bf16", device=cuda)
+        ix.upsert(C[bounds[g]:bounds[g + 1]])
+        assert ix.plan(len(Q), 10)["kernel"] == "qres256"
+        lists.append(ix.query_keys(Q, 10, row_base=bounds[g]))
+        torch.cuda.synchronize()
+        ix.close()
+    s, r, _ = merge_topk_keys(torch.stack(lists, dim=1), 10)
+    np.testing.assert_array_equal(r.cpu().numpy(), fr)
+    np.testing.assert_array_equal(s.cpu().numpy(), fs)
+
+
+def test_qres_concurrent_streams(cuda):
+    """Two workspaces on two streams through the register-resident plan == the batches one by one
+    (the fragment-major query copy is per workspace)."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(29)
+    C = _clustered(rng, 40000, 768)
+    Qs = [torch.from_numpy(_clustered(rng, B, 768)).to(cuda) for B in (1024, 700, 1024, 512)]
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ix.set_debug_flags(QRES)
+    serial = [[t.cpu().numpy() for t in ix.query(q, 10)] for q in Qs]
+    streams = [torch.cuda.current_stream(cuda), torch.cuda.Stream(device=cuda)]
+    streams[1].wait_stream(streams[0])
+    outs = []
+    for rep in range(3):
+        for i, q in enumerate(Qs):
+            ix.set_workspace(i % 2)
+            outs.append(ix.query(q, 10, stream=streams[i % 2]))
+    torch.cuda.synchronize()
+    ix.set_workspace(0)
+    ix.close()
+    for j, (s, r) in enumerate(outs):
+        np.testing.assert_array_equal(r.cpu().numpy(), serial[j % len(Qs)][1])
+        np.testing.assert_array_equal(s.cpu().numpy(), serial[j % len(Qs)][0])

@@ -14,7 +14,7 @@ import re
 
 
 def short(name: str) -> str:
-    m = re.search(r"ahr::(?:dense|graph)::(\w+)(<[^>]*>)?", name)
+    m = re.search(r"ahr::(?:dense|graph)::(?:qres::)?(\w+)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:50]
 
 
