@@ -2258,8 +2258,11 @@ __device__ __forceinline__ int f32_perm(int j) { return (j & ~7) | ((j & 1) << 2
 // on each 1-KiB piece in turn. Same arithmetic and order as the loop: the per-lane fma chain in j
 // order, then the butterfly. `row` may be global or LDS (topk_small_kernel converts its queries
 // in place); [0, d_pad) is written in full, zeros past dim.
+// frag (optional): also write the register-resident kernel's fragment-major query copy (ahr_qres.h
+// launch_frag's layouts) for query q: frag_mode 32 = 32x32x16 form, 16 = 16x16x32 form.
 __device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, int dim, int normalize,
-                                                 uint8_t* row, int d_pad, int dt, int lane) {
+                                                 uint8_t* row, int d_pad, int dt, int lane, uint8_t* frag = nullptr,
+                                                 int64_t q = 0, int frag_mode = 0) {
   f32x4 v[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -2288,17 +2291,40 @@ __device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, in
 #pragma unroll
       for (int e = 0; e < 4; ++e) w4[e] = w4[e] / nrm;
     }
+    uint2 w;
     if (dt == DT_BF16) {
-      uint2 w;
       w.x = (uint32_t)f32_to_bf16_rne(w4[0]) | ((uint32_t)f32_to_bf16_rne(w4[1]) << 16);
       w.y = (uint32_t)f32_to_bf16_rne(w4[2]) | ((uint32_t)f32_to_bf16_rne(w4[3]) << 16);
-      *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
     } else {
-      _Float16* o = reinterpret_cast<_Float16*>(row) + j;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (_Float16)w4[e];
+      w.x = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)w4[0]) |
+            ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)w4[1]) << 16);
+      w.y = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)w4[2]) |
+            ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)w4[3]) << 16);
+    }
+    *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
+    if (frag) {  // the 4 elements stay inside one 16-B chunk of the fragment-major copy
+      int64_t o;
+      if (frag_mode == 16)
+        o = (((q >> 4) * (d_pad >> 5) + (j >> 5)) * 64 + (q & 15) + 16 * ((j >> 3) & 3)) * 16 + (j & 7) * 2;
+      else
+        o = (((q >> 5) * (d_pad >> 4) + (j >> 4)) * 64 + (q & 31) + 32 * ((j >> 3) & 1)) * 16 + (j & 7) * 2;
+      *reinterpret_cast<uint2*>(frag + o) = w;
     }
   }
+}
+
+// Query conversion for the register-resident plan: the convert kernel's rows (the pre-pass reads
+// them) plus the fragment-major copy the qres kernel loads, in one launch (bf16/f16, dim % 4 == 0,
+// d_pad <= 1024: convert_row_fast's shape).
+__global__ __launch_bounds__(256) void convert_queries_frag_kernel(const float* __restrict__ src, int64_t n, int dim,
+                                                                   int normalize, uint8_t* __restrict__ dst,
+                                                                   int64_t row_stride, int d_pad, int dt,
+                                                                   uint8_t* __restrict__ frag, int frag_mode) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+  if (i >= n) return;
+  convert_row_fast(src + i * dim, dim, normalize, dst + i * row_stride, d_pad, dt, lane, frag, i, frag_mode);
 }
 
 // fp32 rows -> storage rows (one wave per row): optional L2 normalisation, dtype conversion,
@@ -3730,11 +3756,29 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   int st = ensure_query_ws(ix, B, k, s);
   if (st) return st;
   prof_mark(ix, 0, s);
-  const bool small_plan = k <= AHR_MAX_K && ix->count > 0 && plan_search(ix, B, k).kernel == KERNEL_SMALL;
-  if (!(small_plan && small_fuses_convert(ix)))
+  const int pre_kernel = k <= AHR_MAX_K && ix->count > 0 ? plan_search(ix, B, k).kernel : -1;
+  const bool small_plan = pre_kernel == KERNEL_SMALL;
+  // the register-resident plan's fragment-major query copy (qbuf_kb: the k-blocked copy's buffer)
+  bool frag_done = false;
+  if (pre_kernel == KERNEL_QRES) {
+    if (!ix->qbuf_kb) {
+      if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
+        return fail(AHR_ENOMEM, "query workspace allocation failed");
+      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
+    }
+    if (small_fuses_convert(ix)) {  // one launch: rows + fragments
+      hipLaunchKernelGGL(convert_queries_frag_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B,
+                         ix->dim, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, ix->dtype, ix->qbuf_kb,
+                         qres::frag_mode(k, ix->debug_flags));
+      frag_done = true;
+    }
+  }
+  if (!frag_done && !(small_plan && small_fuses_convert(ix)))
     hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
                        (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                        ix->row_stride, ix->d_pad, ix->dtype);
+  if (pre_kernel == KERNEL_QRES && !frag_done)
+    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, k, ix->qbuf_kb, ix->debug_flags, s);
   if (k > AHR_MAX_K) {
     switch (ix->dtype) {
       case AHR_BF16: return run_query_large_k<DT_BF16>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);
@@ -3769,15 +3813,6 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     const int64_t chunks = (int64_t)B * n_kb * 4;
     hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->qbuf,
                        ix->row_stride, (int64_t)0, (int64_t)B, n_kb, ix->qbuf_kb);
-  }
-  if (p.kernel == KERNEL_QRES && ix->count > 0) {
-    // the register-resident kernel's B operand: a fragment-major copy of the converted queries
-    if (!ix->qbuf_kb) {
-      if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
-        return fail(AHR_ENOMEM, "query workspace allocation failed");
-      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
-    }
-    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, k, ix->qbuf_kb, ix->debug_flags, s);
   }
   // single searches (the drop-in's search() and environment resets): the small kernels merge the
   // splits in their last workgroup, no merge launch

@@ -99,16 +99,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
+// tile_rsrc from a base the compiler cannot prove uniform (it then wraps every load in a
+// readfirstlane waterfall loop): the halves are made uniform explicitly (callers guarantee it)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc_u(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)bytes);
+  return tile_rsrc(reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo), n);
+}
+
 __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
                                            0, 0);
 }
 
-// the same with a compile-time byte offset (the instruction's 12-bit immediate: no extra VGPR)
-template <int IMM>
-__device__ __forceinline__ void blds16_imm(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
-  static_assert(IMM >= 0 && IMM < 4096, "buffer instruction offset field");
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, IMM,
+// the same with a wave-uniform byte offset added to the global address only, through soffset (an
+// SGPR; the instruction's immediate offset would also shift the LDS destination)
+__device__ __forceinline__ void blds16_soff(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff, 0,
                                            0);
 }
 

@@ -24,6 +24,10 @@ bool supported(int dtype, int d_pad_bytes, int k);
 void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes, int k, uint8_t* qfrag, int flags,
                  hipStream_t s);
 
+// The fragment layout the planned form reads: 16 (16x16x32 form) or 32 (32x32x16 form), for the
+// fused conversion (convert_queries_frag_kernel) that writes it directly.
+int frag_mode(int k, int flags);
+
 // One fused launch: part_keys [B][n_splits][k] (the merge kernels' input), thr [B] optional
 // admission seeds. grid = n_splits * qblocks; n_splits % 8 == 0 when flags has the XCD remap bit.
 void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,

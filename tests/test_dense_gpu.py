@@ -216,18 +216,20 @@ def test_default_plans(cuda):
     assert ix.plan(16, 10)["kernel"] == "small"
     assert ix.plan(17, 10)["kernel"] == "tilelane128"
     assert ix.plan(1, 17)["kernel"] == "tile128"
-    assert ix.plan(2048, 10)["kernel"] == "qkv128"
-    assert ix.plan(6144, 10)["kernel"] == "qkv128"
+    assert ix.plan(2048, 10)["kernel"] == "qres256"
+    assert ix.plan(6144, 10)["kernel"] == "qres256"
+    assert ix.plan(2048, 13)["kernel"] == "qkv128"  # k beyond the register-resident kernel
     assert ix.plan(1024, 17)["kernel"] == "tile128"
     ix.set_debug_flags(4096)
     assert ix.plan(1024, 10)["kernel"] == "qkv128"
-    ix.set_debug_flags(2048)  # without the query-resident kernel
+    ix.set_debug_flags(2048)  # without the query-resident kernels
     assert ix.plan(1024, 10)["kernel"] == "tilelane128"
     assert ix.plan(6144, 10)["kernel"] == "lane256"
     ix.close()
     ix = DenseIndex(768, 400000, dtype="f16", device=cuda)  # seed samples < 1/32 of the rows
     ix.upsert(np.zeros((300000, 768), np.float32))
-    assert ix.plan(4096, 10)["kernel"] == "tilelane128"
+    assert ix.plan(4096, 10)["kernel"] == "qres256"
+    assert ix.plan(4096, 13)["kernel"] == "tilelane128"
     ix.close()
     ix = DenseIndex(1024, 1000, dtype="bf16", device=cuda)  # not a query-resident dimension
     assert ix.plan(1024, 10)["kernel"] == "tilelane128"

@@ -189,3 +189,27 @@ def test_qres_concurrent_streams(cuda):
     for j, (s, r) in enumerate(outs):
         np.testing.assert_array_equal(r.cpu().numpy(), serial[j % len(Qs)][1])
         np.testing.assert_array_equal(s.cpu().numpy(), serial[j % len(Qs)][0])
+
+
+@pytest.mark.parametrize("dim,normalize", [(766, False), (768, True), (764, True)])
+def test_qres_query_conversion_paths(cuda, dim, normalize):
+    """dim % 4 == 0 converts the queries and writes the kernel's fragment-major copy in one launch;
+    other dims (same d_pad = 768) take the conversion kernel plus the separate fragment copy: both
+    must give the tile kernel's answer, with and without query normalisation."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(41 + dim)
+    C = _clustered(rng, 40000, dim)
+    Q = rng.standard_normal((700, dim)).astype(np.float32) * (3.0 if normalize else 1.0)
+    if not normalize:
+        Q = dr.normalize_rows(Q)
+    ix = DenseIndex(dim, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    outs = []
+    for flags, kernel in ((QRES, "qres256"), (QRES | QRES16, "qres256"), (T256, "t256"), (TILELANE, "tilelane128")):
+        ix.set_debug_flags(flags)
+        assert ix.plan(len(Q), 10)["kernel"] == kernel
+        outs.append([t.cpu().numpy() for t in ix.query(Q, 10, normalize=normalize)])
+    ix.close()
+    for a, b in ((outs[0], outs[3]), (outs[1], outs[2])):
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[0], b[0])

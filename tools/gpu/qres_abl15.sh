@@ -1,0 +1,9 @@
+# 16x16x32 form: staging cost split (ablation build).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+AHR_LIB_PATH=ah-rag_amd/ah_rag/_lib/ablation/libahr_hip.so timeout -k 10 400 python -u tools/dense_ablation.py --batches 1024 --rounds 3 \
+  --variants p16:-1:268435456,max16:-1:268435712,st16:-1:402653184,p32:-1:0,tl:-1:32 \
+  > gpurun_out/qres_ablation16.log 2>&1 || { echo ABL_FAILED; tail -30 gpurun_out/qres_ablation16.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/qres_ablation16.log | tail -1
