@@ -3195,13 +3195,13 @@ bool qkv_ok(const ahr_index* ix, int B, int k) {
 // query rows (or one group's lane lists of the end merge) within LDS; not under a kernel flag.
 bool small_ok(const ahr_index* ix, int B, int k) {
   if (ix->dtype == AHR_F32)  // exact mode: the VALU fma-chain stream (topk_small_f32_kernel)
-    return B <= smallf32::kMaxQ && k <= 16 && ix->d_pad <= 1024 && !(ix->debug_flags & kKernelFlags);
+    return B <= smallf32::kMaxQ && k <= 16 && ix->d_pad <= 1024 && !(ix->debug_flags & kForceFlags);
   if (B > small::kMaxQ || k > 16) return false;
   // 2 and 4 query groups: the per-lane list inserts (nearly every score of a lane's short stream)
   // outweigh the saved pre-pass (hotpot90k: 51 us at B = 32, 81 us at B = 64, vs the 128x128
   // lane-local kernel's ~40 us with its pre-pass), so only under the ablation flag
   if (B > 16 && !(ix->debug_flags & kFlagSmallWide)) return false;
-  if (ix->debug_flags & kKernelFlags) return false;
+  if (ix->debug_flags & kForceFlags) return false;
   return small::lds_bytes(ix->row_stride, 16, small::groups(B)) <= 160 * 1024;
 }
 
@@ -3215,7 +3215,7 @@ bool kb256_ok(const ahr_index* ix, int B, int k) {
   if (k > 16 || ix->dtype == AHR_F32 || B <= 0) return false;
   if (ix->debug_flags & (kFlagNoKB256 | kFlagKB128)) return false;
   if (ix->debug_flags & kFlagKB256) return true;
-  if (ix->debug_flags & kKernelFlags) return false;  // another kernel explicitly requested
+  if (ix->debug_flags & kForceFlags) return false;  // another kernel explicitly requested
   return ix->count >= kKB256MinRows;
 }
 
@@ -3233,9 +3233,11 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
   if (!qres::supported(ix->dtype, ix->d_pad * ix->elem, k) || B <= 0) return false;
   if (ix->debug_flags & kFlagNoQres) return false;
   if (ix->debug_flags & kFlagQres) return true;
-  if (ix->debug_flags & kKernelFlags) return false;  // another kernel explicitly requested
+  if (ix->debug_flags & kForceFlags) return false;  // another kernel explicitly requested
+  // from kKB256MinRows on the corpus streams from HBM and the k-blocked kernel stays ahead (5M x 768
+  // f16, B = 1024: 7.49 vs 7.71 ms per launch on the same box)
   const int S = sample_rows_for(ix);
-  return B >= kQresMinBatch && S > 0 && ix->count >= 4 * (int64_t)S;
+  return B >= kQresMinBatch && S > 0 && ix->count >= 4 * (int64_t)S && ix->count < kKB256MinRows;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
@@ -4070,7 +4072,7 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
                              kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold |
                              kFlagNoBarrier | kFlagNoLdsRead | kFlagQresStagger | kFlagQresScreenLoop |
-                             kFlagQres16);
+                             kFlagQres16 | kFlagQres4w);
   return AHR_OK;
 }
 

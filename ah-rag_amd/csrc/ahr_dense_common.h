@@ -189,6 +189,7 @@ enum {
   kFlagQresStagger = 1 << 26,     // qres kernel: waves 4-7 one stage behind waves 0-3 (A/B; same results)
   kFlagQresScreenLoop = 1 << 27,  // qres kernel: pass-mask + select-chain screening (A/B; same results)
   kFlagQres16 = 1 << 28,          // qres: the 16x16x32 form (k <= 10; A/B)
+  kFlagQres4w = 1 << 29,          // qres: the 16x16x32 form with 4 waves of 64 queries, 1 per SIMD (k <= 10; A/B)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
@@ -197,6 +198,8 @@ constexpr bool kAblation = false;
 #endif
 constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
                              kFlagKB256 | kFlagNoKB256 | kFlagKB128 | kFlagQres;
+// the flags that request a kernel (the kFlagNo* ones only take one out of the plan)
+constexpr int kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 }  // namespace dense

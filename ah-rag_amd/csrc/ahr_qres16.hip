@@ -25,20 +25,32 @@ namespace qres {
 // start): 72 KiB, and 88 KiB of lane buffers.
 // =============================================================================================
 constexpr int kSlots16 = 3;
+#ifndef AHR_QRES_PRE4
+#define AHR_QRES_PRE4 1
+#endif
+constexpr int kPre4 = AHR_QRES_PRE4;  // G = 4: the k32 step the previous block's screening precedes
 
-template <int NKT>
+template <int NKT, int W>
 struct Cfg16 {
   static constexpr int kSK = NKT / 2;           // k-tiles per stage
   static constexpr int kStage = kSK * kKt;      // 24 KiB at d_pad = 768
   static constexpr int kPieces = kSK * 4;
-  static_assert(kPieces % kWaves == 0, "equal DMA share per wave");
-  static constexpr int kPPW = kPieces / kWaves;
+  static_assert(kPieces % W == 0, "equal DMA share per wave");
+  static constexpr int kPPW = kPieces / W;
   static constexpr int kNS = NKT * 2;           // k32 steps
   static constexpr int kSS = kSK * 2;           // k32 steps per stage
-  static constexpr int kOffBuf = kSlots16 * kStage;  // [g][kLaneCap][512 lanes] u64
-  static constexpr int kLds = kOffBuf + 2 * kLaneCap * kThreads * 8;
+  static constexpr int kOffBuf = kSlots16 * kStage;  // [g][kLaneCap][64 W lanes] u64, G * W = 16
+  static constexpr int kLds = kOffBuf + kLaneCap * 16 * 64 * 8;
 };
-static_assert(Cfg16<12>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
+static_assert(Cfg16<12, 8>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 template <int DT>
 __device__ __forceinline__ void mfma16(const u32x4& a, const u32x4& b, f32x4& acc) {
@@ -62,12 +74,17 @@ __global__ __launch_bounds__(256) void frag16_kernel(const uint8_t* __restrict__
   *reinterpret_cast<u32x4*>(qfrag + i * 16) = v;
 }
 
-template <int DT, int NKT, int KCAP, int ABL>
-__global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
+// G query groups of 16 per wave: G = 2 (8 waves, 2 per SIMD, 256 VGPRs each) or G = 4 (4 waves,
+// 1 per SIMD with 512 registers: 64 resident queries, each A fragment read from LDS feeds 8 MFMAs
+// instead of 4, and the previous block's screening runs inside the next block's MFMA stream).
+template <int DT, int NKT, int KCAP, int ABL, int G>
+__global__ __launch_bounds__(64 * (16 / G)) __attribute__((amdgpu_waves_per_eu(4 / G, 4 / G))) void topk_qres16_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
     int qblocks, int flags) {
-  using C = Cfg16<NKT>;
+  constexpr int W = 16 / G;      // waves
+  constexpr int NT = 64 * W;     // threads
+  using C = Cfg16<NKT, W>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -90,17 +107,17 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
   const int b_begin = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n_blocks / n_splits));
   const int b_end = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n_blocks / n_splits));
   const int n_st = 2 * (b_end - b_begin);
-  const int qw0 = qb * kTQ + wave * 32;
+  const int qw0 = qb * kTQ + wave * 16 * G;
   const bool live = qw0 < n_q;  // wave-uniform: a wave past the batch only stages and syncs
-  float thr[2];
+  float thr[G];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < G; ++g) {
     const int q = qw0 + 16 * g + fr;
     thr[g] = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
   }
 
-  // DMA (the 32x32 kernel's stages): piece p = wave + 8 i is k-tile p / 4 = wave / 4 + 2 i, rows
-  // 8 (wave % 4) .. +8: the pieces of a wave differ by 2 k-tiles (256 B: soffset, no extra VGPR)
+  // DMA (the 32x32 kernel's stages): piece p = wave + W i is k-tile p / 4 = wave / 4 + (W / 4) i,
+  // rows 8 (wave % 4) .. +8: the pieces of a wave differ by W / 4 k-tiles (soffset, no extra VGPR)
   const int d_row = 8 * (wave & 3) + (lane >> 3);
   const uint32_t src_off = (uint32_t)(d_row * row_stride) + (wave >> 2) * kRowBytes +
                            ((((lane & 7) ^ ((d_row >> 1) & 7))) << 4);
@@ -113,32 +130,51 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
         tile_rsrc_u(corpus + (int64_t)b * kTR * row_stride + (st & 1) * C::kSK * kRowBytes, blk_bytes);
     unsigned char* slot = slot_of(st) + dst_off;
 #pragma unroll
-    for (int i = 0; i < C::kPPW; ++i) blds16_soff(r, src_off, i * 2 * kRowBytes, slot + i * 2 * kKt);
+    for (int i = 0; i < C::kPPW; ++i)
+      blds16_soff(r, src_off, i * (W / 4) * kRowBytes, slot + i * (W / 4) * kKt);
   };
   if (n_st > 0) issue(0);
   if (n_st > 1) issue(1);
 
   // resident B fragments: k32 step S of query group g
-  u32x4 qf[C::kNS][2];
+  // (two arrays of 2 groups: SROA leaves a single [24][4] array of 1.5 KiB in private memory)
+  u32x4 qf01[C::kNS][2];
+  u32x4 qf23[C::kNS][G == 4 ? 2 : 1];
+#define QF(S, g) (*((g) < 2 ? &qf01[S][(g) & 1] : &qf23[S][((g) & 1) % (G == 4 ? 2 : 1)]))
   {
-    const uint8_t* src = qfrag + (int64_t)(qb * 16 + wave * 2) * C::kNS * 1024 + lane * 16;
+    const uint8_t* src = qfrag + (int64_t)(qb * 16 + wave * G) * C::kNS * 1024 + lane * 16;
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int S = 0; S < C::kNS; ++S) qf[S][g] = *reinterpret_cast<const u32x4*>(src + (g * C::kNS + S) * 1024);
+      for (int S = 0; S < C::kNS; ++S) QF(S, g) = *reinterpret_cast<const u32x4*>(src + (g * C::kNS + S) * 1024);
   }
   // consumed here, behind the prologue DMA (see topk_qres_kernel)
 #pragma unroll
-  for (int S = 0; S < C::kNS; ++S) {
-    asm volatile("" : "+v"(qf[S][0]));
-    asm volatile("" : "+v"(qf[S][1]));
-  }
-  asm volatile("" : "+v"(thr[0]), "+v"(thr[1]));
+  for (int S = 0; S < C::kNS; ++S)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (g < 2)
+        asm volatile("" : "+v"(QF(S, g)));
+      else  // G = 4: query groups 2, 3 in AGPRs (MFMA B operands read them directly)
+        asm volatile("" : "+a"(QF(S, g)));
+    }
+#pragma unroll
+  for (int g = 0; g < G; ++g) asm volatile("" : "+v"(thr[g]));
+  auto thr_at = [&](int g) __attribute__((always_inline)) {  // runtime g (thr[g] would go to scratch)
+    float t = thr[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) {
+      float tj = thr[j];
+      asm volatile("" : "+v"(tj));  // a select of values, not of addresses (InstCombine would fold it)
+      t = g == j ? tj : t;
+    }
+    return t;
+  };
   // Admission is by score alone (score >= thr): a score equal to the threshold whose row would lose
   // the tie is buffered too and dropped by the next compaction or the final sort (no key threshold
   // in registers: the VGPR budget is spent on the resident queries).
 
-  // Per (lane, query group g) LDS area of kLaneCap 8-B slots, slot c at lb[(g * kLaneCap + c) * kThreads]
+  // Per (lane, query group g) LDS area of kLaneCap 8-B slots, slot c at lb[(g * kLaneCap + c) * NT]
   // (a wave's 64 lanes hit 64 consecutive u64). The split's first passing block of a lane-query is
   // staged raw — its 8 scores in slots 0-3 (2 per slot), its first row in slot 4 — with 5 stores and
   // no per-score work; a staged score leaves the candidates through a dead bit. Scores of later
@@ -151,11 +187,20 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
   constexpr int kStageKeys = kLaneCap - 5;
   static_assert(kLaneCap - 1 - kStageKeys == 4 && kLaneCap - 1 <= 10,
                 "key mode: at most k_out <= 10 keys, the staged survivors land in slots 4..1");
-  // per-lane state in one register (the VGPR budget is the resident queries'): bit g: block staged,
-  // bits [4 + 4 g, +4): keys, bits [16 + 8 g, +8): dead staged scores
+  // per-lane state (the VGPR budget is the resident queries'): stg bit g: block staged, bits
+  // [4 + 4 g, +4): keys; dead staged scores in 8 bits per g: stg bits [16 + 8 g) at G = 2, dm at G = 4
   uint32_t stg = 0;
+  uint32_t dm = 0;
+  constexpr int kDeadSh = G == 2 ? 16 : 0;
   auto nk = [&](int g) __attribute__((always_inline)) { return (int)((stg >> (4 + 4 * g)) & 0xF); };
-  auto slot = [&](int g, int c) __attribute__((always_inline)) { return lb + (g * kLaneCap + c) * kThreads; };
+  auto dead_of = [&](int g) __attribute__((always_inline)) {
+    return ((G == 2 ? stg : dm) >> (kDeadSh + 8 * g)) & 0xFFu;
+  };
+  auto set_dead = [&](int g, uint32_t d) __attribute__((always_inline)) {
+    uint32_t& r = G == 2 ? stg : dm;
+    r = (r & ~(0xFFu << (kDeadSh + 8 * g))) | (d << (kDeadSh + 8 * g));
+  };
+  auto slot = [&](int g, int c) __attribute__((always_inline)) { return lb + (g * kLaneCap + c) * NT; };
   auto key_slot = [&](int g, int i) __attribute__((always_inline)) { return slot(g, kLaneCap - 1 - i); };
   // row of staged score j (slot j / 2, half j % 2) = acc[rh][g][r] with rh = j / 4, r = j % 4
   auto row_of = [&](int r0, int j) __attribute__((always_inline)) {
@@ -170,10 +215,10 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
   // threshold. A staged block still holding live scores with the keys full has at most
   // k_out - kStageKeys <= 4 of them (k_out <= 10): they become keys 6.. in slots 4, 3, .. — read in
   // pair order 3, 2, 1, 0, a slot is only overwritten once its pair is read or holds no live score.
-  auto overflow = [&](int g) {
+  auto overflow = [&](int g) __attribute__((always_inline)) {
     const bool stgd = stg & (1u << g);
     int n = nk(g);
-    uint32_t dead = stgd ? (stg >> (16 + 8 * g)) & 0xFF : 0xFF;
+    uint32_t dead = stgd ? dead_of(g) : 0xFFu;
     const int r0s = stgd ? (int)(uint32_t)*slot(g, 4) : 0;
     const float t = thr[g];
 #pragma unroll 1
@@ -228,25 +273,28 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
       stg &= ~(1u << g);
       dead = 0xFF;
     }
-    stg = (stg & ~((0xFu << (4 + 4 * g)) | (0xFFu << (16 + 8 * g)))) | ((uint32_t)n << (4 + 4 * g)) |
-          ((stg & (1u << g)) ? dead << (16 + 8 * g) : 0u);
+    stg = (stg & ~(0xFu << (4 + 4 * g))) | ((uint32_t)n << (4 + 4 * g));
+    set_dead(g, (stg & (1u << g)) ? dead : 0u);
   };
   // a finished block: per query group g the lane's 8 scores acc[rh][g][r], rows r0 + 16 rh + 4 fq + r
-  auto screen = [&](const f32x4 (&acc)[2][2], int r0) __attribute__((always_inline)) {
-    bool pass[2];
+  auto screen = [&](const f32x4 (&acc)[2][G], int r0) __attribute__((always_inline)) {
+    bool pass[G];
+    bool any = false;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < G; ++g) {
       const float m = fmaxf(fmaxf(fmaxf(acc[0][g][0], acc[0][g][1]), fmaxf(acc[0][g][2], acc[0][g][3])),
                             fmaxf(fmaxf(acc[1][g][0], acc[1][g][1]), fmaxf(acc[1][g][2], acc[1][g][3])));
       pass[g] = m >= thr[g];
+      any = any || pass[g];
     }
-    if (!__builtin_amdgcn_ballot_w64(pass[0] || pass[1])) return;  // wave-uniform: the common case
+    if (!__builtin_amdgcn_ballot_w64(any)) return;  // wave-uniform: the common case
     if constexpr ((ABL & ABL_MAXONLY) != 0) {  // cost split: the maxima and the ballot only
       asm volatile("" ::"v"(thr[0]));
       return;
     }
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    // (compile-time g: a loop this large is not unrolled, and thr would be indexed at run time)
+    static_for<0, G>([&](auto GI) __attribute__((always_inline)) {
+      constexpr int g = decltype(GI)::value;
       if (pass[g]) {
         if (!(stg & (1u << g)) && nk(g) == 0) {  // the split's first passing block: stage it raw
 #pragma unroll
@@ -261,16 +309,22 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
             for (int j = 0; j < 8; ++j)
               if (row_of(r0, j) >= (uint32_t)n_rows) dead |= 1u << j;
           }
-          stg |= (1u << g) | (dead << (16 + 8 * g));
-        } else {  // rare: per-score keys (a loop, so the slow path is one copy of code)
-          if constexpr ((ABL & ABL_STAGEONLY) != 0) continue;
+          stg |= 1u << g;
+          set_dead(g, dead);
+        } else {  // rare: keys for the passing scores only (one loop trip per passing score)
+          if constexpr ((ABL & ABL_STAGEONLY) != 0) return;
+          uint32_t pm = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pm |= (acc[j >> 2][g][j & 3] >= thr[g] ? 1u : 0u) << j;
 #pragma unroll 1
-          for (int jj = 0; jj < 8; ++jj) {
+          while (pm) {
+            const int jj = __builtin_ctz(pm);
+            pm &= pm - 1;
             float v = acc[0][g][0];
 #pragma unroll
             for (int j2 = 1; j2 < 8; ++j2) v = (jj == j2) ? acc[j2 >> 2][g][j2 & 3] : v;
             const uint32_t row = row_of(r0, jj);
-            if (v >= thr[g] && row < (uint32_t)n_rows) {
+            if (v >= thr[g] && row < (uint32_t)n_rows) {  // (thr may have risen in this loop)
               *key_slot(g, nk(g)) = make_key(v, row_base + row);
               stg += 1u << (4 + 4 * g);
               if (nk(g) == ((stg & (1u << g)) ? kStageKeys : kLaneCap)) overflow(g);
@@ -278,7 +332,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
           }
         }
       }
-    }
+    });
   };
 
   // Sync at the start of stage st: this wave's pieces of stage st landed (st + 1 may stay in
@@ -300,22 +354,25 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
 #pragma unroll
   for (int h = 0; h < 2; ++h) a_off[h] = fr * kRowBytes + (((4 * h + fq) ^ ((fr >> 1) & 7)) << 4);
   auto frag = [&](const unsigned char* slot, int s, int rh) __attribute__((always_inline)) {
-    if constexpr ((ABL & ABL_NOREAD) != 0) return qf[(s + 5) % C::kNS][rh];
+    if constexpr ((ABL & ABL_NOREAD) != 0) return QF((s + 5) % C::kNS, rh);
     return *reinterpret_cast<const u32x4*>(slot + (s >> 1) * kKt + rh * 16 * kRowBytes + a_off[s & 1]);
   };
   u32x4 fa[2][2];  // [buffer][rh]: step t + 1 in flight while step t multiplies
-  f32x4 acc[2][2];
+  f32x4 acc[2][G];
+  f32x4 accp[2][G];  // the previous block's scores while its screening runs (G = 4)
   // one stage: 12 k32 steps, step t prefetches step t + 1 of the same stage; `pre` (the previous
-  // block's screening: acc is overwritten only by the first MFMA) runs first
+  // block's screening) runs before step kPre: at G = 2 first (acc is overwritten only by the first
+  // MFMA, no second register set), at G = 4 behind the first steps' MFMAs, which it overlaps
+  constexpr int kPre = G == 4 ? kPre4 : 0;
   auto stage = [&](auto H, int st, auto&& pre) __attribute__((always_inline)) {
     constexpr int h = decltype(H)::value;
     const unsigned char* slot = slot_of(st);
-    pre();
+    if (kPre == 0) pre();
 #pragma unroll
     for (int rh = 0; rh < 2; ++rh) fa[0][rh] = frag(slot, 0, rh);
-#pragma unroll
-    for (int t = 0; t < C::kSS; ++t) {
-      if (t + 1 < C::kSS) {
+    auto step = [&](auto T) __attribute__((always_inline)) {
+      constexpr int t = decltype(T)::value;
+      if constexpr (t + 1 < C::kSS && (kPre == 0 || t + 1 != kPre)) {
 #pragma unroll
         for (int rh = 0; rh < 2; ++rh) fa[(t + 1) & 1][rh] = frag(slot, t + 1, rh);
       }
@@ -323,60 +380,74 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
 #pragma unroll
       for (int rh = 0; rh < 2; ++rh)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          if (h == 0 && t == 0) {
+        for (int g = 0; g < G; ++g) {
+          if constexpr (h == 0 && t == 0) {
             f32x4 z = {};
-            mfma16<DT>(fa[0][rh], qf[0][g], z);
+            mfma16<DT>(fa[0][rh], QF(0, g), z);
             acc[rh][g] = z;
           } else {
-            mfma16<DT>(fa[t & 1][rh], qf[h * C::kSS + t][g], acc[rh][g]);
+            mfma16<DT>(fa[t & 1][rh], QF(h * C::kSS + t, g), acc[rh][g]);
           }
         }
       __builtin_amdgcn_sched_barrier(0);
+    };
+    // (compile-time steps: a loop holding the screening would not be unrolled, and the resident
+    // fragments would be indexed at run time, from private memory)
+    static_for<0, kPre>(step);
+    if constexpr (kPre > 0) {  // (step kPre's fragments are read after it: 8 registers fewer live)
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rh = 0; rh < 2; ++rh) fa[kPre & 1][rh] = frag(slot, kPre, rh);
     }
+    static_for<kPre, C::kSS>(step);
   };
   // a finished block's top-k screening, run after the NEXT block's first barrier, so no wave waits
   // at a barrier for another wave's survivors (the partner wave's MFMAs fill the SIMD meanwhile)
-  auto finish = [&](int b) __attribute__((always_inline)) {
+  auto finish = [&](const f32x4 (&a)[2][G], int b) __attribute__((always_inline)) {
     if constexpr ((ABL & ABL_NOSCREEN) != 0) {  // GEMM only: every chain kept live (rule 17), no top-k
 #pragma unroll
       for (int rh = 0; rh < 2; ++rh)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) asm volatile("" ::"v"(acc[rh][g]));
+        for (int g = 0; g < G; ++g) asm volatile("" ::"v"(a[rh][g]));
     } else {
-      screen(acc, b * kTR);
+      screen(a, b * kTR);
     }
   };
-  auto nothing = []() {};
+  auto nothing = []() __attribute__((always_inline)) {};
 #pragma unroll 1
   for (int b = b_begin; b < b_end; ++b) {
     const int st0 = 2 * (b - b_begin);
     stage_sync(st0);
     if (live) {
-      if (b > b_begin)
-        stage(std::integral_constant<int, 0>{}, st0, [&]() { finish(b - 1); });
-      else
+      if (b > b_begin) {
+#pragma unroll
+        for (int rh = 0; rh < 2; ++rh)
+#pragma unroll
+          for (int g = 0; g < G; ++g) accp[rh][g] = acc[rh][g];
+        stage(std::integral_constant<int, 0>{}, st0, [&]() __attribute__((always_inline)) { finish(accp, b - 1); });
+      } else
         stage(std::integral_constant<int, 0>{}, st0, nothing);
     }
     stage_sync(st0 + 1);
     if (live) stage(std::integral_constant<int, 1>{}, st0 + 1, nothing);
   }
-  if (live && b_end > b_begin) finish(b_end - 1);
+  if (live && b_end > b_begin) finish(acc, b_end - 1);
 
   // each lane sorts its two areas (the query registers are dead by now): keys plus a staged block's
   // scores at or above the threshold; per query the 4 lane quarters' lists meet in the idle ring,
   // quarter 0 merges them and writes the (query, split) list
   uint64_t* xch = reinterpret_cast<uint64_t*>(smem);  // [quarter 1..3][query-local 256][KCAP]
 #pragma unroll 1
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < G; ++g) {
     uint64_t L[KCAP];
 #pragma unroll
     for (int j = 0; j < KCAP; ++j) L[j] = 0;
 #pragma unroll 1
     for (int c = 0; c < nk(g); ++c) list_insert<KCAP>(L, *key_slot(g, c));
     if (stg & (1u << g)) {
-      const float tg = g ? thr[1] : thr[0];  // (thr[g] with a runtime g would put thr in scratch)
-      const uint32_t dead = (stg >> (16 + 8 * g)) & 0xFF;
+      const float tg = thr_at(g);
+      const uint32_t dead = dead_of(g);
       const int r0s = (int)(uint32_t)*slot(g, 4);
 #pragma unroll 1
       for (int jj = 0; jj < 8; ++jj) {
@@ -384,7 +455,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
         if (!((dead >> jj) & 1) && v >= tg) list_insert<KCAP>(L, make_key(v, row_base + row_of(r0s, jj)));
       }
     }
-    const int qlx = wave * 32 + 16 * g + fr;
+    const int qlx = wave * 16 * G + 16 * g + fr;
     __syncthreads();  // the ring (and, for g = 1, the previous exchange) is free
     if (fq) {
 #pragma unroll
@@ -410,7 +481,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres16_kernel(
   }
 }
 
-template <int DT, int KCAP, int ABL = 0>
+#undef QF
+
+template <int DT, int KCAP, int G, int ABL = 0>
 void launch16_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, hipStream_t s) {
   if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
@@ -419,7 +492,7 @@ void launch16_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, i
                     ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0) | ((flags & kFlagMaxOnly) ? ABL_MAXONLY : 0) |
                     ((flags & kFlagQresScreenLoop) ? ABL_STAGEONLY : 0);  // (the switch is the 32x32 form's A/B)
 #define AHR_QRES_ABL(V) \
-  case V: launch16_t<DT, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s); return;
+  case V: launch16_t<DT, KCAP, G, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       AHR_QRES_ABL(32) AHR_QRES_ABL(64)
@@ -427,11 +500,12 @@ void launch16_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, i
     }
 #undef AHR_QRES_ABL
   }
-  constexpr auto kern = &topk_qres16_kernel<DT, 12, KCAP, ABL>;
-  static_assert(3 * kTQ * KCAP * 8 <= kSlots16 * Cfg16<12>::kStage, "end exchange must fit the ring");
+  using C = Cfg16<12, 16 / G>;
+  constexpr auto kern = &topk_qres16_kernel<DT, 12, KCAP, ABL, G>;
+  static_assert(3 * kTQ * KCAP * 8 <= kSlots16 * C::kStage, "end exchange must fit the ring");
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), Cfg16<12>::kLds);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), Cfg16<12>::kLds, s, rows, qfrag,
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), C::kLds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(64 * (16 / G)), C::kLds, s, rows, qfrag,
                      row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags);
 }
 
@@ -445,17 +519,24 @@ void launch_frag16(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_byt
 void launch16(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
               uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
               hipStream_t s) {
+  const bool w4 = flags & kFlagQres4w;
+#define AHR_QRES16_GO(DT, KC)                                                                                        \
+  (w4 ? launch16_t<DT, KC, 4>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks,    \
+                              flags, s)                                                                              \
+      : launch16_t<DT, KC, 2>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks,    \
+                              flags, s))
   if (dtype == AHR_BF16) {
     if (k <= 8)
-      launch16_t<DT_BF16, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+      AHR_QRES16_GO(DT_BF16, 8);
     else
-      launch16_t<DT_BF16, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+      AHR_QRES16_GO(DT_BF16, 12);
   } else {
     if (k <= 8)
-      launch16_t<DT_F16, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+      AHR_QRES16_GO(DT_F16, 8);
     else
-      launch16_t<DT_F16, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+      AHR_QRES16_GO(DT_F16, 12);
   }
+#undef AHR_QRES16_GO
 }
 
 }  // namespace qres

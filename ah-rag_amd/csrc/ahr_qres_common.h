@@ -32,8 +32,8 @@ enum { ABL_NOSCREEN = 1, ABL_NOLOADS = 2, ABL_NOWAIT = 4, ABL_NOBARRIER = 8, ABL
 
 constexpr int kLaneCap = 11;  // 16x16x32 form: keys per (lane, query); k <= 10 leaves one free slot
 
-// the 16x16x32 form on request (k <= 10: its lane buffers); the 32x32x16 form by default
-inline bool use16(int k, int flags) { return k < kLaneCap && (flags & kFlagQres16); }
+// the 16x16x32 forms on request (k <= 10: their lane buffers); the 32x32x16 form by default
+inline bool use16(int k, int flags) { return k < kLaneCap && (flags & (kFlagQres16 | kFlagQres4w)); }
 
 // ahr_qres16.hip
 void launch_frag16(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes, uint8_t* qfrag, hipStream_t s);

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 QRES = 1 << 23      # plan the register-resident kernel wherever it applies
 QRES16 = 1 << 28    # ... in its 16x16x32 form
+QRES4W = 1 << 29    # ... in its 16x16x32 form with 4 waves of 64 queries
 TILELANE = 32       # the lane-local 128x128 tile kernel at any batch
 T256 = 32768        # the 256x256 16x16x32 tile kernel
 
@@ -45,10 +46,11 @@ def _check_forms(ix, Q, k):
     d = _run(ix, Q, k, TILELANE, "tilelane128")
     np.testing.assert_array_equal(a[1], d[1])
     np.testing.assert_array_equal(a[0], d[0])
-    c = _run(ix, Q, k, QRES | QRES16, "qres256")
     ref = _run(ix, Q, k, T256, "t256") if k <= 10 else a
-    np.testing.assert_array_equal(c[1], ref[1])
-    np.testing.assert_array_equal(c[0], ref[0])
+    for form in (QRES16, QRES4W):
+        c = _run(ix, Q, k, QRES | form, "qres256")
+        np.testing.assert_array_equal(c[1], ref[1])
+        np.testing.assert_array_equal(c[0], ref[0])
     return a
 
 
@@ -132,7 +134,7 @@ def test_qres_ties_order_by_row(cuda):
     pick = rng.integers(0, 300, 600)
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
-    for flags, k in ((QRES, 10), (QRES, 12), (QRES | QRES16, 10)):
+    for flags, k in ((QRES, 10), (QRES, 12), (QRES | QRES16, 10), (QRES | QRES4W, 10)):
         s, r = _run(ix, base[pick], k, flags, "qres256")
         np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(k)[None, :])
         assert (s == s[:, :1]).all()
@@ -205,7 +207,8 @@ def test_qres_query_conversion_paths(cuda, dim, normalize):
     ix = DenseIndex(dim, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     outs = []
-    for flags, kernel in ((QRES, "qres256"), (QRES | QRES16, "qres256"), (T256, "t256"), (TILELANE, "tilelane128")):
+    for flags, kernel in ((QRES, "qres256"), (QRES | QRES16, "qres256"), (QRES | QRES4W, "qres256"), (T256, "t256"),
+                          (TILELANE, "tilelane128")):
         ix.set_debug_flags(flags)
         assert ix.plan(len(Q), 10)["kernel"] == kernel
         outs.append([t.cpu().numpy() for t in ix.query(Q, 10, normalize=normalize)])
