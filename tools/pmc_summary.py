@@ -6,7 +6,10 @@ Per kernel and per launch (mean over launches):
     staging loads are exactly that pattern;
   * HBM write bytes = WRITE_SIZE (KiB) x 1024       — exact for 16-B stores; our partial-list stores
     are 8 B/lane (uncalibrated width, reported as measured);
-  * MFMA work from SQ_INSTS_VALU_MFMA_MOPS_BF16 and the kernel duration from the kernel trace.
+  * MFMA work from SQ_INSTS_VALU_MFMA_MOPS_BF16 / _F16 (bf16 / f16 launches) and the matrix-core
+    busy cycles SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1024 SIMDs: 16 per 16x16x32 MFMA, 32 per
+    32x32x16), as a fraction of 1024 SIMDs x the traced duration x the 2.4 GHz peak clock;
+  * the kernel duration from the kernel trace.
 Infinity-Cache hits are counted inside FETCH_SIZE (the counter sits on the L2's memory side), so
 "HBM" here means "beyond L2".
 
@@ -32,7 +35,7 @@ def _rows(pattern: str):
 
 
 def _short(name: str) -> str:
-    m = re.search(r"ahr::(?:dense|graph)::(\w+)(<[^>]*>)?", name)
+    m = re.search(r"ahr::(?:dense|graph)::(?:qres::)?(\w+)(<[^>]*>)?", name)
     if not m:
         return name[:60]
     return m.group(1) + (m.group(2) or "")
@@ -76,17 +79,25 @@ def main() -> None:
         if base not in ("topk_tile_kernel", "topk_tilelane_kernel", "topk_lane_kernel", "topk_qkv_kernel", "topk_t256_kernel",
                         "topk_small_kernel", "topk_small_f32_kernel", "merge_block_kernel", "merge_lane_lists_kernel", "merge_heads_kernel",
                         "merge_kernel", "sample_kth_kernel", "convert_rows_kernel", "expand_rerank_kernel",
-                        "expand_kernel", "topk_kb256_kernel", "reblock_kb_kernel", "lca_kernel"):
+                        "expand_kernel", "topk_kb256_kernel", "reblock_kb_kernel", "lca_kernel",
+                        "topk_qres_kernel", "topk_qres16_kernel", "convert_queries_frag_kernel"):
             continue
         rec = out.setdefault(base, {"variants": {}})
         f = fetch.get(k, {}).get("FETCH_SIZE", [])
         w = write.get(k, {}).get("WRITE_SIZE", [])
+        mean = lambda c: (sum(c) / len(c)) if c else None  # noqa: E731
         mf = sq.get(k, {}).get("SQ_INSTS_VALU_MFMA_MOPS_BF16", [])
+        mh = sq.get(k, {}).get("SQ_INSTS_VALU_MFMA_MOPS_F16", [])
+        mb = sq.get(k, {}).get("SQ_VALU_MFMA_BUSY_CYCLES", [])
         v = {"launches": len(f) or len(w),
              "read_bytes_per_launch": (sum(f) / len(f)) * 1024 * 2 if f else None,
              "write_bytes_per_launch": (sum(w) / len(w)) * 1024 if w else None,
-             "mfma_mops_bf16_per_launch": (sum(mf) / len(mf)) if mf else None,
+             "mfma_mops_bf16_per_launch": mean(mf),
+             "mfma_mops_f16_per_launch": mean(mh),
+             "mfma_busy_cycles_per_launch": mean(mb),
              "avg_us_trace": dur.get(k, {}).get("avg_us")}
+        if v["mfma_busy_cycles_per_launch"] and v["avg_us_trace"]:
+            v["mfma_busy_frac"] = round(v["mfma_busy_cycles_per_launch"] / (1024 * v["avg_us_trace"] * 1e-6 * 2.4e9), 4)
         if v["read_bytes_per_launch"] is not None and v["write_bytes_per_launch"] is not None:
             v["hbm_bytes_per_launch"] = v["read_bytes_per_launch"] + v["write_bytes_per_launch"]
         rec["variants"][k] = v

@@ -11,5 +11,5 @@ mkdir -p "$OUT"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" --output-format csv -- python -u bench.py $ARGS > "$OUT/trace.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" --output-format csv -- python -u bench.py $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" --output-format csv -- python -u bench.py $ARGS > "$OUT/write.log" 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/sq" --output-format csv -- python -u bench.py $ARGS > "$OUT/sq.log" 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/sq" --output-format csv -- python -u bench.py $ARGS > "$OUT/sq.log" 2>&1 || exit $?
 echo done
