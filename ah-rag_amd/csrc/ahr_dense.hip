@@ -1913,6 +1913,9 @@ __global__ __launch_bounds__(64) void merge_kernel(const uint64_t* __restrict__ 
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) L[j] = 0;
   for (int64_t i = lane; i < n; i += 64) list_insert<KCAP>(L, src[i]);
+  // lane j keeps output j (k <= 64): one coalesced store per output array at the end instead of a
+  // lane-0 store per round
+  uint64_t mine = 0;
   for (int j = 0; j < k; ++j) {
     const uint64_t best = wave_max_u64(L[0]);
     if (best != 0 && L[0] == best) {
@@ -1920,12 +1923,13 @@ __global__ __launch_bounds__(64) void merge_kernel(const uint64_t* __restrict__ 
       for (int t = 0; t < KCAP - 1; ++t) L[t] = L[t + 1];
       L[KCAP - 1] = 0;
     }
-    if (lane == 0) {
-      const int64_t o = (int64_t)q * k + j;
-      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
-      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
-      if (keys_out) keys_out[o] = best;
-    }
+    mine = lane == j ? best : mine;
+  }
+  if (lane < k) {
+    const int64_t o = (int64_t)q * k + lane;
+    if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
+    if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
+    if (keys_out) keys_out[o] = mine;
   }
 }
 
@@ -1995,6 +1999,9 @@ __global__ __launch_bounds__(64) void merge_lane_lists_kernel(const uint64_t* __
   uint64_t L[KCAP];
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) L[j] = (lane < n_lists && j < k_in) ? src[j] : 0;
+  // lane j keeps output j (k <= 64): one coalesced store per output array at the end instead of a
+  // lane-0 store per round
+  uint64_t mine = 0;
   for (int j = 0; j < k; ++j) {
     const uint64_t best = wave_max_u64(L[0]);
     if (best != 0 && L[0] == best) {
@@ -2002,12 +2009,13 @@ __global__ __launch_bounds__(64) void merge_lane_lists_kernel(const uint64_t* __
       for (int t = 0; t < KCAP - 1; ++t) L[t] = L[t + 1];
       L[KCAP - 1] = 0;
     }
-    if (lane == 0) {
-      const int64_t o = (int64_t)q * k + j;
-      if (scores) scores[o] = best ? key_score(best) : -INFINITY;
-      if (rows) rows[o] = best ? (int32_t)key_row(best) : -1;
-      if (keys_out) keys_out[o] = best;
-    }
+    mine = lane == j ? best : mine;
+  }
+  if (lane < k) {
+    const int64_t o = (int64_t)q * k + lane;
+    if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
+    if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
+    if (keys_out) keys_out[o] = mine;
   }
 }
 
