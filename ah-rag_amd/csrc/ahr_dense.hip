@@ -1333,7 +1333,7 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
     const uint8_t* __restrict__ corpus_kb, const uint8_t* __restrict__ queries_kb, int n_kb, int n_rows, int n_q,
     int n_row_tiles, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
     const float* __restrict__ thr_init, int n_splits, int qblocks, int flags, uint64_t* __restrict__ cand_keys,
-    int cand_cap) {
+    int cand_cap, uint32_t* __restrict__ prog, uint32_t epoch, int lead) {
   static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
   using C = KbCfg<WN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1428,6 +1428,50 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
       if (kth) thr[nb] = fmaxf(thr[nb], key_score(kth));
     };
 
+    // Split pacing (XCD-remapped grid of 256, one workgroup per CU): the 32 workgroups of an XCD
+    // (8 splits x 4 query blocks) share that XCD's 4-MiB L2 -- a split's corpus tile is read by its
+    // 4 query blocks, a query block's k-blocks by 8 splits -- and left alone they drift apart by
+    // several tiles, so each line is fetched from HBM ~2x (r02: 17 GB per launch vs 7.68 GB of
+    // corpus at C3). Every 4 k-steps a workgroup publishes its step (plain store: the line stays
+    // in the XCD's L2) and wave 0 reads its 31 siblings' steps with two scalar loads (glc: from
+    // L2; counted by lgkmcnt, so the DMA ring's vmcnt waits are untouched), holding the workgroup
+    // at the barrier while any sibling is more than kLead steps behind. Values carry the launch's
+    // epoch (another launch's are "not started"); a finished workgroup publishes 0xFFFFF. The
+    // wait is bounded: after kMaxSpins polls (a sibling not resident, e.g. a concurrent kernel
+    // holds its CU) the workgroup stops pacing for the rest of the launch.
+    constexpr int kMaxSpins = 1024;
+    const int kLead = lead;
+    const bool pace = prog != nullptr && lead > 0 && gridDim.x == 256 && (flags & kFlagXcdRemap) && !(flags & kFlagKbNoPace);
+    const uint32_t ep = (epoch & 0xFFFu) << 20;
+    uint32_t* const prog_x = prog + (blockIdx.x & 7) * 32;  // this XCD's 32 slots
+    // a plain global store (a volatile one becomes a flat store followed by a vmcnt(0) drain)
+    __attribute__((address_space(1))) uint32_t* const prog_g =
+        (__attribute__((address_space(1))) uint32_t*)(prog_x + (blockIdx.x >> 3));
+    bool paced = pace;
+    // The sibling steps are loaded one pacing interval ahead (issued after a barrier, read before
+    // the next pacing barrier), so the scalar-load latency stays off the barrier path; only a
+    // sibling that is behind makes wave 0 re-read them synchronously.
+    typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
+    u32x16 pa = {}, pb = {};
+    auto poll_issue = [&]() __attribute__((always_inline)) {
+      asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\ts_load_dwordx16 %1, %2, 0x40 glc"
+                   : "=s"(pa), "=s"(pb)
+                   : "s"(prog_x)
+                   : "memory");
+    };
+    auto slowest = [&](bool fresh) __attribute__((always_inline)) {
+      if (fresh) poll_issue();
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pa), "+s"(pb)::"memory");
+      const u32x16 a = pa, b = pb;
+      int m = 0x7FFFFFFF;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int va = (a[j] & 0xFFF00000u) == ep ? (int)(a[j] & 0xFFFFFu) : -1;
+        const int vb = (b[j] & 0xFFF00000u) == ep ? (int)(b[j] & 0xFFFFFu) : -1;
+        m = min(m, min(va, vb));
+      }
+      return m;
+    };
     constexpr int kAhead = C::kStages - 1;  // k-steps in flight ahead of the one being multiplied
     const int pro = total < kAhead ? total : kAhead;
     for (int c = 0; c < pro; ++c) issue(c, c);
@@ -1453,8 +1497,22 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
             wait_vmcnt<0>();
         }
       }
+      if (paced && (c & 3) == 0 && c >= kLead && wave_u == 0) {
+        int spins = 0;
+        for (bool fresh = false; slowest(fresh) < c - kLead; fresh = true) {
+          if (++spins > kMaxSpins) {
+            paced = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
+      }
       lds_barrier();  // everyone's step c landed; everyone finished reading step c - 1
+      // the step store goes before the step's DMA issue: whether stores retire in order with the
+      // loads or early, the next counted wait still covers all of step c + 1's pieces
+      if (pace && (c & 3) == 0 && wave_u == 0 && lane == 0) *prog_g = ep | (uint32_t)c;
       if (c + kAhead < total && !((flags & kFlagNoLoads) && c >= 1)) issue(c + kAhead, st_i);  // into step c - 1's stage
+      if (paced && (c & 3) == 0 && wave_u == 0) poll_issue();  // read at the next pacing point
       const unsigned char* st = smem + st_c * C::kStageBytes;
       st_c = st_c + 1 == C::kStages ? 0 : st_c + 1;
       st_i = st_i + 1 == C::kStages ? 0 : st_i + 1;
@@ -1549,6 +1607,7 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
         for (int nb = 0; nb < 4; ++nb) sink += acc[mb][nb][0] + acc[mb][nb][3];
       if (sink == 1234.5678f) part_keys[0] = 1;
     }
+    if (pace && wave_u == 0 && lane == 0) *prog_g = ep | 0xFFFFFu;  // done: never behind
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   }
 
@@ -3100,7 +3159,7 @@ struct ahr_index {
   uint8_t* qbuf_kb = nullptr;
   int64_t q_cap = 0;  // rows in qbuf (multiple of kRowPad)
   uint64_t* part = nullptr;
-  int64_t part_cap = 0;  // uint64 elements (+ 8 more: the small kernels' fold counter, fold_ctr())
+  int64_t part_cap = 0;  // uint64 elements (+ 8: the small kernels' fold counter; + 128: kb256 pacing)
   float* sample = nullptr;  // pre-pass scores [B][S] then thresholds [B]
   int64_t sample_cap = 0;   // floats
   uint8_t* cand = nullptr;  // query-resident kernel: candidate groups (counts, row bases, scores)
@@ -3118,6 +3177,9 @@ struct ahr_index {
   int prof_max_calls = 0;
   int prof_calls = 0;
   uint32_t* fold_ctr() const { return reinterpret_cast<uint32_t*>(part + part_cap); }
+  // kb256 split pacing: 8 XCDs x 32 step slots behind the fold counter, and the launch epoch
+  uint32_t* kb_pace() const { return reinterpret_cast<uint32_t*>(part + part_cap + 8); }
+  mutable uint32_t kb_epoch = 0;
 };
 
 namespace {
@@ -3377,10 +3439,10 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
     ix->part = nullptr;
     ix->part_cap = 0;
-    if (hipMalloc(&ix->part, (p_need + 8) * sizeof(uint64_t)) != hipSuccess)
+    if (hipMalloc(&ix->part, (p_need + 8 + 128) * sizeof(uint64_t)) != hipSuccess)
       return fail(AHR_ENOMEM, "partial top-k workspace allocation failed");
     ix->part_cap = p_need;
-    AHR_HIP(hipMemsetAsync(ix->part + p_need, 0, 8 * sizeof(uint64_t), s));  // fold counter
+    AHR_HIP(hipMemsetAsync(ix->part + p_need, 0, (8 + 128) * sizeof(uint64_t), s));  // fold counter, kb pace
   }
   const int64_t s_need = (int64_t)B * (kGroupMax + 1);
   if (s_need > ix->sample_cap) {
@@ -3476,6 +3538,18 @@ void launch_t256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
                      thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
 
+// kb256 split pacing lead in k-steps (AHR_KB_PACE_LEAD; default 0 = off). Measured at C3 (5M x
+// 768 f16, B = 1024, one box, alternating): lead 12 cuts the bytes beyond L2 from 13.5 to 10.6 GB
+// per launch (1.76x -> 1.38x of the corpus) but costs 4-5 % (7.71-7.80 -> 8.09-8.10 ms): the
+// kernel is bound by its MFMA/DMA-issue core, not by HBM, and pacing adds waits.
+inline int kb_pace_lead() {
+  static const int lead = [] {
+    const char* e = getenv("AHR_KB_PACE_LEAD");
+    return e ? atoi(e) : 0;
+  }();
+  return lead;
+}
+
 template <int DT, int KCAP, int WN>
 void launch_kb256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                   const float* thr, int flags, hipStream_t s) {
@@ -3485,7 +3559,8 @@ void launch_kb256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, i
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), C::kLds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(C::kThreads), C::kLds, s, ix->rows_kb,
                      ix->qbuf_kb, ix->d_pad * ix->elem / kb256::kKB, n_rows, B, p.n_row_tiles, row_base, k, ix->part,
-                     thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
+                     thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p),
+                     ix->kb_pace(), ++ix->kb_epoch, kb_pace_lead());
 }
 
 template <int DT, int NKT>
@@ -4080,7 +4155,7 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
                              kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold |
                              kFlagNoBarrier | kFlagNoLdsRead | kFlagQresStagger | kFlagQresScreenLoop |
-                             kFlagQres16 | kFlagQres4w);
+                             kFlagQres16 | kFlagQres4w | kFlagKbNoPace);
   return AHR_OK;
 }
 

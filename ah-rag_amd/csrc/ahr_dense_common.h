@@ -190,6 +190,7 @@ enum {
   kFlagQresScreenLoop = 1 << 27,  // qres kernel: pass-mask + select-chain screening (A/B; same results)
   kFlagQres16 = 1 << 28,          // qres: the 16x16x32 form (k <= 10; A/B)
   kFlagQres4w = 1 << 29,          // qres: the 16x16x32 form with 4 waves of 64 queries, 1 per SIMD (k <= 10; A/B)
+  kFlagKbNoPace = 1 << 30,        // kb256: no split pacing (A/B; same results)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
