@@ -334,8 +334,9 @@ class DenseIndex:
         256x256 16x16x32 kernel (bf16/f16, k <= 16), 65536 = the small-batch kernel up to B = 64,
         1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
         1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 768, k <= 12),
+        1 << 28 / 1 << 29 = its 16x16x32 forms (k <= 10), 1 << 30 = kb256 without split pacing,
         1 << 20 / 1 << 21 = k-blocked kernels read every tile from tile 0 / the split's first
-        tile (garbage)."""
+        tile (garbage). The garbage-result switches need the ablation build."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
 
     _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256", "kb128",

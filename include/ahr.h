@@ -131,10 +131,16 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
  * 65536 = the small-batch streaming kernel up to B = 64, 131072 = the k-blocked 256x256 kernel
  * wherever it applies, 262144 = never the k-blocked kernels, 524288 = the k-blocked 256x128 kernel
  * (two workgroups per CU) wherever it applies, 4194304 = small batches merge through a merge
- * launch instead of the last-workgroup fold, 16384 = tilelane without the cross-tile prefetch.
+ * launch instead of the last-workgroup fold, 16384 = tilelane without the cross-tile prefetch,
+ * 1 << 23 = the 256-query register-resident kernel (qres256) wherever it applies (bf16/f16,
+ * d_pad 768, k <= 12), 1 << 26 = qres256 with waves 4-7 one stage behind, 1 << 27 = qres256's
+ * select-chain screening, 1 << 28 / 1 << 29 = qres256's 16x16x32 forms (8 waves x 32 queries /
+ * 4 waves x 64 queries; k <= 10), 1 << 30 = kb256 without split pacing. 2048 keeps the
+ * query-resident kernels (qkv and qres256) out of the plan.
  * Cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
  * only, 512 = operands of the first tile only, 1024 = loads never waited for, 1048576 / 2097152 =
- * k-blocked tiles read from tile 0 / the split's first tile) are accepted only by the ablation
+ * k-blocked tiles read from tile 0 / the split's first tile, 1 << 24 / 1 << 25 = qres256 without
+ * stage barriers / LDS fragment reads) are accepted only by the ablation
  * build (-DAHR_ABLATION, __graft_entry__.build_ablation); the shipped library returns AHR_EUNSUP. */
 int ahr_index_set_debug_flags(ahr_index* ix, int flags);
 
@@ -143,7 +149,9 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags);
  * (k <= 16, B >= 6144), 2 = 256x128 lane kernel, 3 = 128x128 lane-local tile kernel (k <= 16,
  * B < 6144), 5 = query-resident kernel (bf16/f16, 2048 <= B <= 8192), 6 = 256x256 16x16x32
  * kernel (opt-in), 7 = small-batch streaming kernel (bf16/f16, B <= 16, k <= 16), 8 = k-blocked
- * 256x256 kernel (bf16/f16, k <= 16, from 512k corpus rows), 9 = k-blocked 256x128 kernel (opt-in). */
+ * 256x256 kernel (bf16/f16, k <= 16, from 512k corpus rows), 9 = k-blocked 256x128 kernel (opt-in),
+ * 10 = 256-query register-resident kernel (bf16/f16, d_pad 768, k <= 12, B >= 512, below 512k
+ * rows, with the threshold pre-pass). */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 
