@@ -47,7 +47,8 @@ struct Cfg {
   static constexpr int kNS = NKT * 4;          // k16 steps = query fragments per lane
   static constexpr int kSS = kSK * 4;          // k16 steps per stage
   static constexpr int kOffBuf = kSlots * kStage;
-  static constexpr int kLds = kOffBuf + kBufCap * kThreads * 8;
+  static constexpr int kOffCnt = kOffBuf + kBufCap * kThreads * 8;  // the P2P stage counter
+  static constexpr int kLds = kOffCnt + 16;
 };
 static_assert(Cfg<12>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
 
@@ -65,7 +66,9 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
 }
 
 
-template <int DT, int NKT, int KCAP, bool STAGGER, int SCR, int ABL>
+// SYNC: 0 = a workgroup barrier per stage (default), 1 = the same with waves 4-7 one stage
+// behind (A/B), 2 = point-to-point stage counter in LDS instead of the barrier (A/B).
+template <int DT, int NKT, int KCAP, int SYNC, int SCR, int ABL>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
@@ -190,6 +193,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
           if (v >= thr && (!ragged || row < (uint32_t)n_rows)) {
             const uint64_t key = make_key(v, row_base + row);
             if (key > thk) {
+              if (nb == kBufCap) compact();  // k_out + 4 > kBufCap (k = 12): one more cut mid-quad
               lbuf[nb * kThreads] = key;
               ++nb;
             }
@@ -239,7 +243,52 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // Sync j: this wave's pieces of stage j landed (stage j + 1 may stay in flight), then the
   // barrier: everyone's stage j landed, and everyone is done with stage j - 2 (waves 4-7 finished
   // it in interval j - 1), whose slot takes stage j + 2. A stage is issued two intervals ahead.
+  // SYNC = 2: no barrier. Each wave adds 1 to an LDS counter at every stage start, after its own
+  // pieces of stages j and j + 1 landed (counted vmcnt wait, stage j + 2 in flight), which also
+  // says it is done with stage j - 1. A wave starts stage j once the counter reached 8 j (every
+  // wave started stage j - 1: everyone's stage-j pieces landed and stage j - 2's slot, which
+  // takes stage j + 2, is free): waves may drift apart by one stage, so a wave's screening runs
+  // beside its SIMD partner's MFMAs instead of holding all 8 waves at the next barrier.
+  // (the counter is read and added through inline asm: for compiler-emitted LDS accesses the
+  // waitcnt pass adds a vmcnt(0) — the LDS-DMA writes alias them — which would drain the ring)
+  const uint32_t cnt_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(smem + C::kOffCnt);
+  if constexpr (SYNC == 2) {
+    if (tid == 0) asm volatile("ds_write_b32 %0, %1" ::"v"(cnt_addr), "v"(0u) : "memory");
+    lds_barrier();
+  }
+  // The counter is read ahead (two steps before the end of each stage: cnt_seen) so the check
+  // at the next stage start usually passes without an LDS round trip; the counter only grows,
+  // so a stale value is a safe lower bound. Only a wave that is ahead re-reads it in a tight
+  // loop (bounded, ~1 ms: a counting bug must end the launch with wrong results, not hang).
+  uint32_t cnt_seen = 0;
+  auto read_ahead = [&]() __attribute__((always_inline)) {
+    asm volatile("ds_read_b32 %0, %1" : "=v"(cnt_seen) : "v"(cnt_addr) : "memory");
+  };
+  auto wait_count = [&](uint32_t target) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cnt_seen)::"memory");
+    if (__builtin_amdgcn_readfirstlane(cnt_seen) >= target) return;
+    for (int spin = 0; spin < (1 << 16); ++spin) {
+      uint32_t v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cnt_addr) : "memory");
+      if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+    }
+  };
+  auto stage_sync_p2p = [&](int j) __attribute__((always_inline)) {
+    if (j >= n_st) return;  // the extra interval: the last block's screening only
+    if (j >= 1) wait_count(8u * (uint32_t)j);
+    if (j + 2 < n_st) issue(j + 2);
+    if (j + 1 < n_st)
+      wait_vm<C::kPPW>();
+    else
+      wait_vm<0>();
+    if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(cnt_addr), "v"(1u) : "memory");
+    if (j == 0) wait_count(8u);
+  };
   auto stage_sync = [&](int j) __attribute__((always_inline)) {
+    if constexpr (SYNC == 2) {
+      stage_sync_p2p(j);
+      return;
+    }
     if (!(ABL & ABL_NOWAIT)) {
       if (j + 1 < n_st)
         wait_vm<C::kPPW>();
@@ -258,7 +307,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     return *reinterpret_cast<const u32x4*>(slot + (s >> 2) * kKt + a_row + (((2 * (s & 3) + fh) ^ a_x) << 4));
   };
   static_assert(C::kSS % 3 == 0, "three fragment registers rotate evenly over a stage");
-  const int lag = (STAGGER && wave >= 4) ? 1 : 0;
+  const int lag = (SYNC == 1 && wave >= 4) ? 1 : 0;
   constexpr bool skip_screen = (ABL & ABL_NOSCREEN) != 0;
   f32x16 acc;
   u32x4 fa[3];
@@ -268,6 +317,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 #pragma unroll
     for (int t = 0; t < C::kSS; ++t) {
       if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2);
+      if (SYNC == 2 && t == C::kSS - 2) read_ahead();
       __builtin_amdgcn_sched_barrier(0);
       if (h == 0 && t == 0) {
         f32x16 z = {};
@@ -357,7 +407,7 @@ void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes
   launch_frag16(qbuf, row_stride, B, d_pad_bytes, qfrag, s);
 }
 
-template <int DT, int KCAP, bool STAGGER, int SCR, int ABL = 0>
+template <int DT, int KCAP, int SYNC, int SCR, int ABL = 0>
 void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, hipStream_t s) {
   if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
@@ -365,14 +415,14 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
                     ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0);
 #define AHR_QRES_ABL(V) \
-  case V: launch_t<DT, KCAP, STAGGER, SCR, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s); return;
+  case V: launch_t<DT, KCAP, SYNC, SCR, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       default: break;
     }
 #undef AHR_QRES_ABL
   }
-  constexpr auto kern = &topk_qres_kernel<DT, 12, KCAP, STAGGER, SCR, ABL>;
+  constexpr auto kern = &topk_qres_kernel<DT, 12, KCAP, SYNC, SCR, ABL>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), Cfg<12>::kLds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), Cfg<12>::kLds, s, rows, qfrag,
@@ -383,11 +433,13 @@ template <int DT, int KCAP>
 void launch_s(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, hipStream_t s) {
   if (flags & kFlagQresStagger)
-    launch_t<DT, KCAP, true, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+    launch_t<DT, KCAP, 1, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+  else if (flags & kFlagQresP2P)
+    launch_t<DT, KCAP, 2, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
   else if (flags & kFlagQresScreenLoop)
-    launch_t<DT, KCAP, false, 0>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+    launch_t<DT, KCAP, 0, 0>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
   else
-    launch_t<DT, KCAP, false, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+    launch_t<DT, KCAP, 0, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
 }
 
 void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
