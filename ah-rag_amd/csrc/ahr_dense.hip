@@ -4155,7 +4155,7 @@ int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
   ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
                              kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold |
                              kFlagNoBarrier | kFlagNoLdsRead | kFlagQresStagger | kFlagQresScreenLoop |
-                             kFlagQres16 | kFlagQres4w | kFlagKbNoPace | kFlagQresP2P);
+                             kFlagQres16 | kFlagQres4w | kFlagKbNoPace | kFlagQresBlkSync);
   return AHR_OK;
 }
 

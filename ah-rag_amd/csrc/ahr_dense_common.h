@@ -191,7 +191,7 @@ enum {
   kFlagQres16 = 1 << 28,          // qres: the 16x16x32 form (k <= 10; A/B)
   kFlagQres4w = 1 << 29,          // qres: the 16x16x32 form with 4 waves of 64 queries, 1 per SIMD (k <= 10; A/B)
   kFlagKbNoPace = 1 << 30,        // kb256: no split pacing (A/B; same results)
-  kFlagQresP2P = 1 << 31,         // qres (32x32x16 form): stage counter in LDS instead of barriers (A/B)
+  kFlagQresBlkSync = 1 << 31,         // qres (32x32x16 form): one barrier per block instead of per stage (A/B)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in

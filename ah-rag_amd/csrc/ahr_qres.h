@@ -11,7 +11,7 @@ namespace qres {
 
 constexpr int kTQ = 256;     // queries per workgroup: 8 waves x 32
 constexpr int kTR = 32;      // corpus rows per block
-constexpr int kBufCap = 15;  // per-lane survivor buffer (keys) in LDS (15: room for the P2P stage counter)
+constexpr int kBufCap = 16;  // per-lane survivor buffer (keys) in LDS
 
 // bf16 / f16 rows of d_pad_bytes = 1536 (d_pad = 768), k <= 12: what the kernel is built for.
 bool supported(int dtype, int d_pad_bytes, int k);

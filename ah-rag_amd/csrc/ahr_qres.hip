@@ -47,8 +47,7 @@ struct Cfg {
   static constexpr int kNS = NKT * 4;          // k16 steps = query fragments per lane
   static constexpr int kSS = kSK * 4;          // k16 steps per stage
   static constexpr int kOffBuf = kSlots * kStage;
-  static constexpr int kOffCnt = kOffBuf + kBufCap * kThreads * 8;  // the P2P stage counter
-  static constexpr int kLds = kOffCnt + 16;
+  static constexpr int kLds = kOffBuf + kBufCap * kThreads * 8;
 };
 static_assert(Cfg<12>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
 
@@ -67,7 +66,7 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
 
 
 // SYNC: 0 = a workgroup barrier per stage (default), 1 = the same with waves 4-7 one stage
-// behind (A/B), 2 = point-to-point stage counter in LDS instead of the barrier (A/B).
+// behind (A/B), 2 = one barrier per block (A/B).
 template <int DT, int NKT, int KCAP, int SYNC, int SCR, int ABL>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
@@ -243,50 +242,23 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // Sync j: this wave's pieces of stage j landed (stage j + 1 may stay in flight), then the
   // barrier: everyone's stage j landed, and everyone is done with stage j - 2 (waves 4-7 finished
   // it in interval j - 1), whose slot takes stage j + 2. A stage is issued two intervals ahead.
-  // SYNC = 2: no barrier. Each wave adds 1 to an LDS counter at every stage start, after its own
-  // pieces of stages j and j + 1 landed (counted vmcnt wait, stage j + 2 in flight), which also
-  // says it is done with stage j - 1. A wave starts stage j once the counter reached 8 j (every
-  // wave started stage j - 1: everyone's stage-j pieces landed and stage j - 2's slot, which
-  // takes stage j + 2, is free): waves may drift apart by one stage, so a wave's screening runs
-  // beside its SIMD partner's MFMAs instead of holding all 8 waves at the next barrier.
-  // (the counter is read and added through inline asm: for compiler-emitted LDS accesses the
-  // waitcnt pass adds a vmcnt(0) — the LDS-DMA writes alias them — which would drain the ring)
-  const uint32_t cnt_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(smem + C::kOffCnt);
-  if constexpr (SYNC == 2) {
-    if (tid == 0) asm volatile("ds_write_b32 %0, %1" ::"v"(cnt_addr), "v"(0u) : "memory");
-    lds_barrier();
-  }
-  // The counter is read ahead (two steps before the end of each stage: cnt_seen) so the check
-  // at the next stage start usually passes without an LDS round trip; the counter only grows,
-  // so a stale value is a safe lower bound. Only a wave that is ahead re-reads it in a tight
-  // loop (bounded, ~1 ms: a counting bug must end the launch with wrong results, not hang).
-  uint32_t cnt_seen = 0;
-  auto read_ahead = [&]() __attribute__((always_inline)) {
-    asm volatile("ds_read_b32 %0, %1" : "=v"(cnt_seen) : "v"(cnt_addr) : "memory");
-  };
-  auto wait_count = [&](uint32_t target) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cnt_seen)::"memory");
-    if (__builtin_amdgcn_readfirstlane(cnt_seen) >= target) return;
-    for (int spin = 0; spin < (1 << 16); ++spin) {
-      uint32_t v;
-      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cnt_addr) : "memory");
-      if (__builtin_amdgcn_readfirstlane(v) >= target) break;
-    }
-  };
-  auto stage_sync_p2p = [&](int j) __attribute__((always_inline)) {
-    if (j >= n_st) return;  // the extra interval: the last block's screening only
-    if (j >= 1) wait_count(8u * (uint32_t)j);
-    if (j + 2 < n_st) issue(j + 2);
-    if (j + 1 < n_st)
-      wait_vm<C::kPPW>();
-    else
+  // SYNC = 2: one barrier per 32-row block instead of one per stage. At a block's first stage e
+  // a wave waits for ALL its pieces in flight (stages e and e + 1: vmcnt(0)), then the barrier:
+  // everyone's e and e + 1 landed and everyone finished stage e - 1, so e + 2 may take stage
+  // e - 2's slot now and e + 3 stage e - 1's at the block's second stage, which needs neither a
+  // wait nor a barrier. The block's screening (after the barrier) then has two stages of MFMAs,
+  // not one, to even out between the waves before the next barrier; the price is waiting for
+  // stage e + 1 one stage after its issue instead of two.
+  auto stage_sync_blk = [&](int j) __attribute__((always_inline)) {
+    if (!(j & 1)) {
       wait_vm<0>();
-    if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(cnt_addr), "v"(1u) : "memory");
-    if (j == 0) wait_count(8u);
+      lds_barrier();
+    }
+    if (j + 2 < n_st) issue(j + 2);
   };
   auto stage_sync = [&](int j) __attribute__((always_inline)) {
     if constexpr (SYNC == 2) {
-      stage_sync_p2p(j);
+      stage_sync_blk(j);
       return;
     }
     if (!(ABL & ABL_NOWAIT)) {
@@ -317,7 +289,6 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 #pragma unroll
     for (int t = 0; t < C::kSS; ++t) {
       if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2);
-      if (SYNC == 2 && t == C::kSS - 2) read_ahead();
       __builtin_amdgcn_sched_barrier(0);
       if (h == 0 && t == 0) {
         f32x16 z = {};
@@ -434,7 +405,7 @@ void launch_s(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, hipStream_t s) {
   if (flags & kFlagQresStagger)
     launch_t<DT, KCAP, 1, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
-  else if (flags & kFlagQresP2P)
+  else if (flags & kFlagQresBlkSync)
     launch_t<DT, KCAP, 2, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
   else if (flags & kFlagQresScreenLoop)
     launch_t<DT, KCAP, 0, 0>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);

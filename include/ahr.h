@@ -135,7 +135,8 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
  * 1 << 23 = the 256-query register-resident kernel (qres256) wherever it applies (bf16/f16,
  * d_pad 768, k <= 12), 1 << 26 = qres256 with waves 4-7 one stage behind, 1 << 27 = qres256's
  * select-chain screening, 1 << 28 / 1 << 29 = qres256's 16x16x32 forms (8 waves x 32 queries /
- * 4 waves x 64 queries; k <= 10), 1 << 30 = kb256 without split pacing. 2048 keeps the
+ * 4 waves x 64 queries; k <= 10), 1 << 30 = kb256 without split pacing, 1 << 31 = qres256
+ * (32x32x16 form) with one barrier per 32-row block instead of one per stage. 2048 keeps the
  * query-resident kernels (qkv and qres256) out of the plan.
  * Cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
  * only, 512 = operands of the first tile only, 1024 = loads never waited for, 1048576 / 2097152 =

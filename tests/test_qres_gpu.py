@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 QRES = 1 << 23      # plan the register-resident kernel wherever it applies
 QRES16 = 1 << 28    # ... in its 16x16x32 form
 QRES4W = 1 << 29    # ... in its 16x16x32 form with 4 waves of 64 queries
-QRES_P2P = 1 << 31  # ... (32x32x16 form) with an LDS stage counter instead of stage barriers
+QRES_BLK = 1 << 31  # ... (32x32x16 form) with one barrier per block instead of per stage
 TILELANE = 32       # the lane-local 128x128 tile kernel at any batch
 T256 = 32768        # the 256x256 16x16x32 tile kernel
 
@@ -47,7 +47,7 @@ def _check_forms(ix, Q, k):
     d = _run(ix, Q, k, TILELANE, "tilelane128")
     np.testing.assert_array_equal(a[1], d[1])
     np.testing.assert_array_equal(a[0], d[0])
-    e = _run(ix, Q, k, QRES | QRES_P2P, "qres256")
+    e = _run(ix, Q, k, QRES | QRES_BLK, "qres256")
     np.testing.assert_array_equal(e[1], a[1])
     np.testing.assert_array_equal(e[0], a[0])
     ref = _run(ix, Q, k, T256, "t256") if k <= 10 else a
@@ -138,7 +138,7 @@ def test_qres_ties_order_by_row(cuda):
     pick = rng.integers(0, 300, 600)
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
-    for flags, k in ((QRES, 10), (QRES, 12), (QRES | QRES_P2P, 12), (QRES | QRES16, 10), (QRES | QRES4W, 10)):
+    for flags, k in ((QRES, 10), (QRES, 12), (QRES | QRES_BLK, 12), (QRES | QRES16, 10), (QRES | QRES4W, 10)):
         s, r = _run(ix, base[pick], k, flags, "qres256")
         np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(k)[None, :])
         assert (s == s[:, :1]).all()
