@@ -102,7 +102,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_index_probe_seed": ([_P, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
         "ahr_index_plan": ([_P, _I, _I, _P, _P, _P, _P], _I),
         "ahr_index_set_workspace": ([_P, _I], _I),
-        "ahr_index_set_debug_flags": ([_P, _I], _I),
+        "ahr_index_set_debug_flags": ([_P, ctypes.c_uint32], _I),
         "ahr_index_query": ([_P, _P, _I, _I, _I, _P, _P, _P], _I),
         "ahr_index_query_keys": ([_P, _P, _I, _I, _I, _L, _P, _P], _I),
         "ahr_index_scores": ([_P, _P, _I, _I, _P, _L, _P], _I),

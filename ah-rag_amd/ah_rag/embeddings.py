@@ -327,20 +327,20 @@ class DenseIndex:
         nat.check(nat.lib().ahr_index_set_seed(self._h, nat.ptr(thr)), "ahr_index_set_seed")
 
     def set_debug_flags(self, flags: int) -> None:
-        """Ablation switches (include/ahr.h): 2 = skip the top-k epilogue (garbage results),
+        """Plan / A/B switches (include/ahr.h; a 32-bit unsigned word, unknown bits refused):
         8 = 128x128 tile kernel (cooperative), 32 = 128x128 lane-local kernel at any batch,
-        64 = 256x128 lane kernel, 256 = group maxima only (garbage), 2048 = plan without the
-        query-resident kernel, 4096 = the query-resident kernel wherever it applies, 32768 = the
-        256x256 16x16x32 kernel (bf16/f16, k <= 16), 65536 = the small-batch kernel up to B = 64,
+        2048 = plan without the query-resident kernels, 4096 = the query-resident (qkv) kernel
+        wherever it applies, 16384 = tilelane without the cross-tile prefetch, 32768 = the 256x256
+        16x16x32 kernel (bf16/f16, k <= 16), 131072 / 262144 = always / never the k-blocked kernel,
         1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
-        1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 768, k <= 12),
-        1 << 28 / 1 << 29 = its 16x16x32 forms (k <= 10), 1 << 30 = kb256 without split pacing,
-        1 << 20 / 1 << 21 = k-blocked kernels read every tile from tile 0 / the split's first
-        tile (garbage). The garbage-result switches need the ablation build."""
-        nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags)), "ahr_index_set_debug_flags")
+        1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768,
+        k <= 12), 1 << 26 = that kernel seeded by the sampled pre-pass instead of seeding itself.
+        Garbage-result cost-split switches (2, 256, 512, 1024, 1 << 20, 1 << 21, 1 << 24, 1 << 25)
+        need the ablation build."""
+        nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags) & 0xFFFFFFFF), "ahr_index_set_debug_flags")
 
-    _KERNELS = ("tile128", "lane256", "lane256x128", "tilelane128", "(removed)", "qkv128", "t256", "small", "kb256", "kb128",
-                "qres256")
+    _KERNELS = ("tile128", "lane256", "(retired)", "tilelane128", "(retired)", "qkv128", "t256", "small", "kb256",
+                "(retired)", "qres256")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

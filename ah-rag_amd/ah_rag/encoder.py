@@ -123,6 +123,10 @@ class TorchEncoder:
             self.pretrained = False
         self.model = self.model.to(device=self.device, dtype=dtype).eval()
         self.dim = int(self.model.config.hidden_size)
+        # the checkpoint's own pad id (MPNet / RoBERTa vocabularies pad with 1: their id 0 is the
+        # <s> token every sequence starts with); BERT and the seeded stand-in pad with 0
+        pad = getattr(self.model.config, "pad_token_id", None)
+        self.pad_id = int(pad) if pad is not None else PAD_ID
 
     def get_sentence_embedding_dimension(self) -> int:
         return self.dim
@@ -141,11 +145,14 @@ class TorchEncoder:
             for s in range(0, len(order), batch_size):
                 sel = order[s:s + batch_size]
                 L = max(len(ids[i]) for i in sel)
-                tok = np.full((len(sel), L), PAD_ID, np.int64)
+                tok = np.full((len(sel), L), self.pad_id, np.int64)
                 for j, i in enumerate(sel):
                     tok[j, :len(ids[i])] = ids[i]
                 tok_t = torch.from_numpy(tok).to(self.device, non_blocking=True)
-                mask = tok_t != PAD_ID
+                # the mask from the sequence lengths, not from token values (a real token may
+                # share the pad id)
+                lens = torch.as_tensor([len(ids[i]) for i in sel], device=self.device)
+                mask = torch.arange(L, device=self.device).unsqueeze(0) < lens.unsqueeze(1)
                 h = self.model(input_ids=tok_t, attention_mask=mask.to(torch.long)).last_hidden_state
                 m = mask.unsqueeze(-1).to(torch.float32)
                 pooled = (h.float() * m).sum(1) / m.sum(1).clamp_min(1e-9)  # mean pooling in fp32

@@ -671,14 +671,16 @@ class HierarchicalGraph:
                      return_cluster: bool = False, db_path: Optional[str] = None,
                      model_name: Optional[str] = None, query_vectors: Optional[np.ndarray] = None) -> List[Any]:
         """search() over many queries with one device pass (B = len(queries))."""
-        if top_k > nat.AHR_MAX_K_LARGE:
-            raise ValueError(f"top_k={top_k} exceeds the dense index limit ({nat.AHR_MAX_K_LARGE})")
         params = resolve_search_params(self.G.graph.get("search_params", {}), top_k, member_top_m, alpha, beta,
                                        gamma, delta, judge_overall_min, confidence_min, type_filter)
         vi = self.G.graph.get("vector_index") if isinstance(self.G.graph.get("vector_index"), dict) else {}
         db_path = db_path or vi.get("db_path", "vector_db")
         model_name = model_name or vi.get("model", DEFAULT_MODEL)
         engine = self.search_engine(db_path)
+        # Chroma answers n_results > count with every row (:714); only a dense top-k that really
+        # needs more than AHR_MAX_K_LARGE rows is out of this index's range
+        if min(top_k, len(engine.index)) > nat.AHR_MAX_K_LARGE:
+            raise ValueError(f"top_k={top_k} exceeds the dense index limit ({nat.AHR_MAX_K_LARGE})")
         if query_vectors is None:
             enc = self._encoder(model_name)
             # a GPU encoder hands its [B, d] fp32 output over on the device (no host round trip)

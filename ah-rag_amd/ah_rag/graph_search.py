@@ -332,7 +332,9 @@ class SearchEngine:
             stream: Optional[torch.cuda.Stream] = None) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
         """Dense top_k -> expansion -> rerank for a batch. Returns host (rows, scores, result)."""
         k = max(1, params.top_k)
-        k_dense = min(k, nat.AHR_MAX_K_LARGE)
+        # rows past the index count come back as -1 anyway: ask for at most count (Chroma's
+        # n_results clamp), so a small corpus answers any top_k
+        k_dense = min(k, max(1, len(self.index)), nat.AHR_MAX_K_LARGE)
         scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
         if stream is not None:  # the gather below and the host copies run on the current stream
             torch.cuda.current_stream(self.graph.device).wait_stream(stream)

@@ -1333,7 +1333,7 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
     const uint8_t* __restrict__ corpus_kb, const uint8_t* __restrict__ queries_kb, int n_kb, int n_rows, int n_q,
     int n_row_tiles, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
     const float* __restrict__ thr_init, int n_splits, int qblocks, int flags, uint64_t* __restrict__ cand_keys,
-    int cand_cap, uint32_t* __restrict__ prog, uint32_t epoch, int lead) {
+    int cand_cap) {
   static_assert(DT != DT_F32, "fp32 keeps the exact single-chain kernels");
   using C = KbCfg<WN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1428,50 +1428,6 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
       if (kth) thr[nb] = fmaxf(thr[nb], key_score(kth));
     };
 
-    // Split pacing (XCD-remapped grid of 256, one workgroup per CU): the 32 workgroups of an XCD
-    // (8 splits x 4 query blocks) share that XCD's 4-MiB L2 -- a split's corpus tile is read by its
-    // 4 query blocks, a query block's k-blocks by 8 splits -- and left alone they drift apart by
-    // several tiles, so each line is fetched from HBM ~2x (r02: 17 GB per launch vs 7.68 GB of
-    // corpus at C3). Every 4 k-steps a workgroup publishes its step (plain store: the line stays
-    // in the XCD's L2) and wave 0 reads its 31 siblings' steps with two scalar loads (glc: from
-    // L2; counted by lgkmcnt, so the DMA ring's vmcnt waits are untouched), holding the workgroup
-    // at the barrier while any sibling is more than kLead steps behind. Values carry the launch's
-    // epoch (another launch's are "not started"); a finished workgroup publishes 0xFFFFF. The
-    // wait is bounded: after kMaxSpins polls (a sibling not resident, e.g. a concurrent kernel
-    // holds its CU) the workgroup stops pacing for the rest of the launch.
-    constexpr int kMaxSpins = 1024;
-    const int kLead = lead;
-    const bool pace = prog != nullptr && lead > 0 && gridDim.x == 256 && (flags & kFlagXcdRemap) && !(flags & kFlagKbNoPace);
-    const uint32_t ep = (epoch & 0xFFFu) << 20;
-    uint32_t* const prog_x = prog + (blockIdx.x & 7) * 32;  // this XCD's 32 slots
-    // a plain global store (a volatile one becomes a flat store followed by a vmcnt(0) drain)
-    __attribute__((address_space(1))) uint32_t* const prog_g =
-        (__attribute__((address_space(1))) uint32_t*)(prog_x + (blockIdx.x >> 3));
-    bool paced = pace;
-    // The sibling steps are loaded one pacing interval ahead (issued after a barrier, read before
-    // the next pacing barrier), so the scalar-load latency stays off the barrier path; only a
-    // sibling that is behind makes wave 0 re-read them synchronously.
-    typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
-    u32x16 pa = {}, pb = {};
-    auto poll_issue = [&]() __attribute__((always_inline)) {
-      asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\ts_load_dwordx16 %1, %2, 0x40 glc"
-                   : "=s"(pa), "=s"(pb)
-                   : "s"(prog_x)
-                   : "memory");
-    };
-    auto slowest = [&](bool fresh) __attribute__((always_inline)) {
-      if (fresh) poll_issue();
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pa), "+s"(pb)::"memory");
-      const u32x16 a = pa, b = pb;
-      int m = 0x7FFFFFFF;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int va = (a[j] & 0xFFF00000u) == ep ? (int)(a[j] & 0xFFFFFu) : -1;
-        const int vb = (b[j] & 0xFFF00000u) == ep ? (int)(b[j] & 0xFFFFFu) : -1;
-        m = min(m, min(va, vb));
-      }
-      return m;
-    };
     constexpr int kAhead = C::kStages - 1;  // k-steps in flight ahead of the one being multiplied
     const int pro = total < kAhead ? total : kAhead;
     for (int c = 0; c < pro; ++c) issue(c, c);
@@ -1497,22 +1453,8 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
             wait_vmcnt<0>();
         }
       }
-      if (paced && (c & 3) == 0 && c >= kLead && wave_u == 0) {
-        int spins = 0;
-        for (bool fresh = false; slowest(fresh) < c - kLead; fresh = true) {
-          if (++spins > kMaxSpins) {
-            paced = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(8);
-        }
-      }
       lds_barrier();  // everyone's step c landed; everyone finished reading step c - 1
-      // the step store goes before the step's DMA issue: whether stores retire in order with the
-      // loads or early, the next counted wait still covers all of step c + 1's pieces
-      if (pace && (c & 3) == 0 && wave_u == 0 && lane == 0) *prog_g = ep | (uint32_t)c;
       if (c + kAhead < total && !((flags & kFlagNoLoads) && c >= 1)) issue(c + kAhead, st_i);  // into step c - 1's stage
-      if (paced && (c & 3) == 0 && wave_u == 0) poll_issue();  // read at the next pacing point
       const unsigned char* st = smem + st_c * C::kStageBytes;
       st_c = st_c + 1 == C::kStages ? 0 : st_c + 1;
       st_i = st_i + 1 == C::kStages ? 0 : st_i + 1;
@@ -1607,7 +1549,6 @@ __global__ __launch_bounds__(KbCfg<WN>::kThreads, KbCfg<WN>::kMinBlocks) void to
         for (int nb = 0; nb < 4; ++nb) sink += acc[mb][nb][0] + acc[mb][nb][3];
       if (sink == 1234.5678f) part_keys[0] = 1;
     }
-    if (pace && wave_u == 0 && lane == 0) *prog_g = ep | 0xFFFFFu;  // done: never behind
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   }
 
@@ -2326,10 +2267,10 @@ __device__ __forceinline__ int f32_perm(int j) { return (j & ~7) | ((j & 1) << 2
 // order, then the butterfly. `row` may be global or LDS (topk_small_kernel converts its queries
 // in place); [0, d_pad) is written in full, zeros past dim.
 // frag (optional): also write the register-resident kernel's fragment-major query copy (ahr_qres.h
-// launch_frag's layouts) for query q: frag_mode 32 = 32x32x16 form, 16 = 16x16x32 form.
+// launch_frag's layout) for query q.
 __device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, int dim, int normalize,
                                                  uint8_t* row, int d_pad, int dt, int lane, uint8_t* frag = nullptr,
-                                                 int64_t q = 0, int frag_mode = 0) {
+                                                 int64_t q = 0) {
   f32x4 v[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -2370,11 +2311,7 @@ __device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, in
     }
     *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
     if (frag) {  // the 4 elements stay inside one 16-B chunk of the fragment-major copy
-      int64_t o;
-      if (frag_mode == 16)
-        o = (((q >> 4) * (d_pad >> 5) + (j >> 5)) * 64 + (q & 15) + 16 * ((j >> 3) & 3)) * 16 + (j & 7) * 2;
-      else
-        o = (((q >> 5) * (d_pad >> 4) + (j >> 4)) * 64 + (q & 31) + 32 * ((j >> 3) & 1)) * 16 + (j & 7) * 2;
+      const int64_t o = (((q >> 5) * (d_pad >> 4) + (j >> 4)) * 64 + (q & 31) + 32 * ((j >> 3) & 1)) * 16 + (j & 7) * 2;
       *reinterpret_cast<uint2*>(frag + o) = w;
     }
   }
@@ -2386,12 +2323,13 @@ __device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, in
 __global__ __launch_bounds__(256) void convert_queries_frag_kernel(const float* __restrict__ src, int64_t n, int dim,
                                                                    int normalize, uint8_t* __restrict__ dst,
                                                                    int64_t row_stride, int d_pad, int dt,
-                                                                   uint8_t* __restrict__ frag, int frag_mode) {
+                                                                   uint8_t* __restrict__ frag, uint32_t* __restrict__ epoch) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && epoch) advance_epoch(epoch);  // the next qres launch's tag
   if (i >= n) return;
-  convert_row_fast(src + i * dim, dim, normalize, dst + i * row_stride, d_pad, dt, lane, frag, i, frag_mode);
+  convert_row_fast(src + i * dim, dim, normalize, dst + i * row_stride, d_pad, dt, lane, frag, i);
 }
 
 // fp32 rows -> storage rows (one wave per row): optional L2 normalisation, dtype conversion,
@@ -2592,14 +2530,13 @@ __device__ __forceinline__ void fold_last_arrival(const uint64_t* part_keys, int
 #define AHR_SMALL_KC 8
 #endif
 namespace small {
-constexpr int kMaxQ = 64;      // 4 groups of 16 queries
+constexpr int kMaxQ = 16;      // one group of 16 queries (the kernel is written for NG groups; only NG = 1 is built)
 constexpr int kKC = AHR_SMALL_KC;  // 32-deep k-steps per work item (one register set)
 constexpr int kPitchPad = 16;  // query rows in LDS: pitch = row bytes + 16 (conflict-free reads)
 // waves per workgroup: 8 (A/B at B = 1 / 16, two batches in flight: 45.1 k / 594 k queries/s
 // with 8 waves, 42.9 k / 516 k with 12, 38.2 k / 471 k with 16 — a 16-wave workgroup fills a CU's
 // VGPRs, so the other batch's kernel cannot co-reside; serial latency 8 % higher with 8)
 __host__ __device__ constexpr int waves(int ng) { return ng == 1 ? AHR_SMALL_WAVES : 8; }
-inline int groups(int B) { return B <= 16 ? 1 : (B <= 32 ? 2 : 4); }
 // LDS: the NG * 16 query rows, later overlaid by one group's lane lists (16 x 4 W x KCAP keys)
 inline int lds_bytes(int64_t row_stride, int kcap, int ng) {
   const int64_t q = (int64_t)16 * ng * (row_stride + kPitchPad);
@@ -3140,6 +3077,8 @@ struct ahr_query_ws {
   int64_t sample_cap = 0;
   uint8_t* cand = nullptr;
   int64_t cand_cap = 0;
+  uint64_t* ss = nullptr;  // register-resident plan: self-seeding tag + granules (published maxima, seeds)
+  int64_t ss_cap = 0;
 };
 constexpr int kMaxWorkspaces = 4;
 
@@ -3164,22 +3103,21 @@ struct ahr_index {
   int64_t sample_cap = 0;   // floats
   uint8_t* cand = nullptr;  // query-resident kernel: candidate groups (counts, row bases, scores)
   int64_t cand_cap = 0;     // bytes
+  uint64_t* ss = nullptr;   // register-resident plan: [1] launch tag, [q_cap][kQresMaxSplits] published maxima, [q_cap] seeds
+  int64_t ss_cap = 0;       // uint64 elements
   int sample_rows = -1;     // S; 0 disables the threshold pre-pass, -1 = sample_rows_for(count)
   const float* seed = nullptr;  // caller-supplied admission thresholds [B] (device), replace the pre-pass
-  // The fields above (qbuf .. cand_cap) are the ACTIVE query workspace; the others are parked
+  // The fields above (qbuf .. ss_cap) are the ACTIVE query workspace; the others are parked
   // here (ahr_index_set_workspace swaps them) so batches on different streams never share one.
   ahr_query_ws parked[kMaxWorkspaces];
   int cur_ws = 0;
-  int debug_flags = 0;      // ablation flags (kFlagSkipEpilogue); 0 in production
+  uint32_t debug_flags = 0;  // ablation / plan flags (kFlag*); 0 in production
   // Optional stage timing: a ring of HIP events, kStages+1 per query call, recorded on the
   // call's stream (ahr_index_profile_begin / _end).
   std::vector<hipEvent_t> prof_events;
   int prof_max_calls = 0;
   int prof_calls = 0;
   uint32_t* fold_ctr() const { return reinterpret_cast<uint32_t*>(part + part_cap); }
-  // kb256 split pacing: 8 XCDs x 32 step slots behind the fold counter, and the launch epoch
-  uint32_t* kb_pace() const { return reinterpret_cast<uint32_t*>(part + part_cap + 8); }
-  mutable uint32_t kb_epoch = 0;
 };
 
 namespace {
@@ -3207,13 +3145,13 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
     (void)hipEventRecord(ix->prof_events[(size_t)ix->prof_calls * (kStages + 1) + stage], s);
 }
 
-// ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 2 = lane 256x128,
-// 10 = 256-query register-resident kernel (ahr_qres.hip),
-// 3 = 128x128 lane-local tile kernel, 5 = query-resident kernel (dimension halves over wave pairs);
-// 4 was a one-wave-per-SIMD query-resident kernel (measured slower, removed), 6 = 256x256 16x16x32
-// kernel (opt-in), 7 = small-batch streaming kernel (B <= 16; <= 64 opt-in)
-enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_LANE256Q128 = 2, KERNEL_TILELANE = 3, KERNEL_QKV = 5,
-       KERNEL_T256 = 6, KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_KB128 = 9, KERNEL_QRES = 10 };
+// ahr_index_plan kernel ids: 0 = 128x128 tile kernel, 1 = lane 256x256, 3 = 128x128 lane-local tile
+// kernel, 5 = query-resident kernel (dimension halves over wave pairs), 6 = 256x256 16x16x32 kernel
+// (opt-in), 7 = small-batch streaming kernel (B <= 16), 8 = k-blocked 256x256 kernel, 10 = 256-query
+// register-resident kernel (ahr_qres.hip). Ids 2, 4 and 9 were measured-slower variants (lane
+// 256x128, a one-wave-per-SIMD query-resident kernel, k-blocked 256x128): removed.
+enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_TILELANE = 3, KERNEL_QKV = 5, KERNEL_T256 = 6,
+       KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_QRES = 10 };
 
 struct SearchPlan {
   int kernel;
@@ -3253,26 +3191,21 @@ inline int sample_rows_for(const ahr_index* ix) {
 bool qkv_ok(const ahr_index* ix, int B, int k) {
   const int nkt = ix->d_pad * ix->elem / kRowBytes;
   if (k > 16 || ix->dtype == AHR_F32 || !(nkt == 6 || nkt == 12)) return false;
-  if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagKB128)) return false;
-  if (ix->debug_flags & kFlagQkv) return true;
-  // B <= 8192: at least 4 splits, so a producer's share of the survivors (~10 x N / S per query
-  // on random-order data) fits its candidate buffer
-  const int S = sample_rows_for(ix);
-  return B >= 2048 && B <= 8192 && S > 0 && ix->count <= 32 * (int64_t)S;
+  if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagNoQres)) return false;
+  // opt-in only: the 256-query register-resident kernel covers its batches (B >= 512, k <= 12)
+  return (ix->debug_flags & kFlagQkv) != 0;
 }
 
-// The small-batch streaming kernel: B <= 16 (<= 64 under kFlagSmallWide), bf16/f16, k <= 16, the
+// The small-batch streaming kernel: B <= 16, bf16/f16, k <= 16, the
 // query rows (or one group's lane lists of the end merge) within LDS; not under a kernel flag.
 bool small_ok(const ahr_index* ix, int B, int k) {
   if (ix->dtype == AHR_F32)  // exact mode: the VALU fma-chain stream (topk_small_f32_kernel)
     return B <= smallf32::kMaxQ && k <= 16 && ix->d_pad <= 1024 && !(ix->debug_flags & kForceFlags);
+  // B <= 16: one group of 16 queries. (2 and 4 groups, B <= 64, measured slower than the 128x128
+  // lane-local kernel with its pre-pass — 51 us at B = 32, 81 us at B = 64 vs ~40 us: removed.)
   if (B > small::kMaxQ || k > 16) return false;
-  // 2 and 4 query groups: the per-lane list inserts (nearly every score of a lane's short stream)
-  // outweigh the saved pre-pass (hotpot90k: 51 us at B = 32, 81 us at B = 64, vs the 128x128
-  // lane-local kernel's ~40 us with its pre-pass), so only under the ablation flag
-  if (B > 16 && !(ix->debug_flags & kFlagSmallWide)) return false;
   if (ix->debug_flags & kForceFlags) return false;
-  return small::lds_bytes(ix->row_stride, 16, small::groups(B)) <= 160 * 1024;
+  return small::lds_bytes(ix->row_stride, 16, 1) <= 160 * 1024;
 }
 
 // The k-blocked 256x256 kernel (bf16/f16, k <= 16) from kKB256MinRows corpus rows on: there the
@@ -3283,22 +3216,19 @@ bool small_ok(const ahr_index* ix, int B, int k) {
 constexpr int64_t kKB256MinRows = 1 << 19;
 bool kb256_ok(const ahr_index* ix, int B, int k) {
   if (k > 16 || ix->dtype == AHR_F32 || B <= 0) return false;
-  if (ix->debug_flags & (kFlagNoKB256 | kFlagKB128)) return false;
+  if (ix->debug_flags & kFlagNoKB256) return false;
   if (ix->debug_flags & kFlagKB256) return true;
   if (ix->debug_flags & kForceFlags) return false;  // another kernel explicitly requested
   return ix->count >= kKB256MinRows;
 }
 
-bool kb128_ok(const ahr_index* ix, int B, int k) {
-  if (k > 16 || ix->dtype == AHR_F32 || B <= 0) return false;
-  return (ix->debug_flags & kFlagKB128) != 0;
-}
 
-// The 256-query register-resident kernel (ahr_qres.hip): bf16/f16 at d_pad = 768, k <= 12, from
-// kQresMinBatch queries on, when the threshold pre-pass runs (its admission threshold is the seed
-// until a lane's own k-th best passes it). Debug flags force it (kFlagQres) or keep it out
-// (kFlagNoQres, or any other kernel flag).
+// The 256-query register-resident kernel (ahr_qres.hip): bf16/f16 at d_pad = 768 or 384, k <= 12,
+// from kQresMinBatch queries and kQresMinRows rows on (every split then has the blocks its
+// self-seeding needs), while admission seeding is on (sample rows != 0). Debug flags force it
+// (kFlagQres) or keep it out (kFlagNoQres, or any other kernel flag).
 constexpr int kQresMinBatch = 512;
+constexpr int64_t kQresMinRows = 32768;
 bool qres_ok(const ahr_index* ix, int B, int k) {
   if (!qres::supported(ix->dtype, ix->d_pad * ix->elem, k) || B <= 0) return false;
   if (ix->debug_flags & kFlagNoQres) return false;
@@ -3306,8 +3236,35 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
   if (ix->debug_flags & kForceFlags) return false;  // another kernel explicitly requested
   // from kKB256MinRows on the corpus streams from HBM and the k-blocked kernel stays ahead (5M x 768
   // f16, B = 1024: 7.49 vs 7.71 ms per launch on the same box)
-  const int S = sample_rows_for(ix);
-  return B >= kQresMinBatch && S > 0 && ix->count >= 4 * (int64_t)S && ix->count < kKB256MinRows;
+  return B >= kQresMinBatch && sample_rows_for(ix) > 0 && ix->count >= kQresMinRows && ix->count < kKB256MinRows;
+}
+
+// Self-seeding buffer of the register-resident plan (ahr_qres.hip): the launch tag (advanced on the
+// device by each query conversion), then per query slot of the padded batch one published maximum
+// per split (at most kQresMaxSplits), then one seed. Zeroed when allocated (tag 0 is never a
+// launch's), so a granule is only ever this workspace's own.
+constexpr int64_t kQresMaxSplits = 256;
+int ensure_ss(ahr_index* ix, hipStream_t s) {
+  const int64_t need = 1 + ix->q_cap * (kQresMaxSplits + 1);
+  if (need <= ix->ss_cap) return AHR_OK;
+  if (ix->ss) AHR_HIP(hipFree(ix->ss));
+  ix->ss = nullptr;
+  ix->ss_cap = 0;
+  if (hipMalloc(&ix->ss, need * sizeof(uint64_t)) != hipSuccess)
+    return fail(AHR_ENOMEM, "self-seeding workspace allocation failed");
+  AHR_HIP(hipMemsetAsync(ix->ss, 0, need * sizeof(uint64_t), s));
+  ix->ss_cap = need;
+  return AHR_OK;
+}
+
+// the second query buffer (the register-resident plan's fragment-major copy, or the k-blocked
+// copy of the kb256 plan), zeroed on the caller's stream when allocated
+int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
+  if (ix->qbuf_kb) return AHR_OK;
+  if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
+    return fail(AHR_ENOMEM, "query workspace allocation failed");
+  AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
+  return AHR_OK;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
@@ -3332,7 +3289,7 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     const bool f32 = ix->dtype == AHR_F32;  // 64-row items (a row per lane) vs 16-row blocks
     p.n_row_tiles = (int)cdiv(ix->count, f32 ? 64 : 16);
     p.n_splits = (int)std::max<int64_t>(
-        1, std::min<int64_t>(256, cdiv(p.n_row_tiles, f32 ? smallf32::kWaves : small::waves(small::groups(B)))));
+        1, std::min<int64_t>(256, cdiv(p.n_row_tiles, f32 ? smallf32::kWaves : small::waves(1))));
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     p.xcd_remap = false;
     return p;
@@ -3349,13 +3306,12 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     return p;
   }
-  if (kb128_ok(ix, B, k) || kb256_ok(ix, B, k)) {
-    // 256x256 tiles, one workgroup per CU, or 256x128 tiles, two per CU: one wave of workgroups
-    const bool w128 = kb128_ok(ix, B, k);
-    p.kernel = w128 ? KERNEL_KB128 : KERNEL_KB256;
-    p.qblocks = (int)cdiv(B, w128 ? KbCfg<2>::kTQ : KbCfg<4>::kTQ);
+  if (kb256_ok(ix, B, k)) {
+    // 256x256 tiles, one workgroup per CU: one wave of workgroups
+    p.kernel = KERNEL_KB256;
+    p.qblocks = (int)cdiv(B, KbCfg<4>::kTQ);
     p.n_row_tiles = (int)cdiv(ix->count, kb256::kTR);
-    int want = std::max(1, (w128 ? 512 : 256) / p.qblocks);
+    int want = std::max(1, 256 / p.qblocks);
     want = std::min(want, std::max(1, p.n_row_tiles));
     p.xcd_remap = want >= 8;
     p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
@@ -3375,24 +3331,18 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     return p;
   }
   if (k <= 16 && !(ix->debug_flags & kFlagTile128)) {
-    if (ix->debug_flags & kFlagLane256q128)
-      p.kernel = KERNEL_LANE256Q128;
-
-    else if (B >= kWideMinBatch && !(ix->debug_flags & kFlagTileLane))
+    if (B >= kWideMinBatch && !(ix->debug_flags & kFlagTileLane))
       p.kernel = KERNEL_LANE256;
     else
       p.kernel = KERNEL_TILELANE;
   }
-  if (p.kernel == KERNEL_LANE256 || p.kernel == KERNEL_LANE256Q128) {
-    // Row tile TR, query tile TQ, `per_cu` resident workgroups per CU. One wave of workgroups;
-    // splits a multiple of 8 (rounded down: an extra workgroup would run as a second wave) so
-    // the XCD remap keeps a split's query blocks on one XCD.
-    const int TR = 256;
-    const int TQ = p.kernel == KERNEL_LANE256 ? 256 : 128;
-    const int per_cu = p.kernel == KERNEL_LANE256 ? 1 : 2;
-    p.qblocks = (int)cdiv(B, TQ);
-    p.n_row_tiles = (int)cdiv(ix->count, TR);
-    int want = std::max(1, 256 * per_cu / p.qblocks);
+  if (p.kernel == KERNEL_LANE256) {
+    // 256 x 256 tiles, one resident workgroup per CU. One wave of workgroups; splits a multiple of
+    // 8 (rounded down: an extra workgroup would run as a second wave) so the XCD remap keeps a
+    // split's query blocks on one XCD.
+    p.qblocks = (int)cdiv(B, 256);
+    p.n_row_tiles = (int)cdiv(ix->count, 256);
+    int want = std::max(1, 256 / p.qblocks);
     want = std::min(want, std::max(1, p.n_row_tiles));
     p.xcd_remap = want >= 8;
     p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
@@ -3421,7 +3371,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
     if (ix->qbuf) AHR_HIP(hipFree(ix->qbuf));
     if (ix->qbuf_kb) AHR_HIP(hipFree(ix->qbuf_kb));
     ix->qbuf = ix->qbuf_kb = nullptr;
-    ix->q_cap = 0;
+    ix->q_cap = 0;  // (the self-seeding granules are sized by q_cap: ensure_ss regrows them)
     if (hipMalloc(&ix->qbuf, q_need * ix->row_stride) != hipSuccess)
       return fail(AHR_ENOMEM, "query workspace allocation failed");
     AHR_HIP(hipMemsetAsync(ix->qbuf, 0, q_need * ix->row_stride, s));
@@ -3431,7 +3381,7 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
   const int64_t qblocks = cdiv(B, kTileQ);
   const int64_t max_splits = cdiv(std::max<int64_t>(1, cdiv(kResidentSlots128, qblocks)), 8) * 8;
   const int64_t wide_splits = std::max<int64_t>(1, 512 / cdiv(B, 128));  // >= any plan's
-  const int64_t t256_lists = 2 * std::max<int64_t>(1, 512 / cdiv(B, 128));  // (split, row half) lists: kb128 >= kb256
+  const int64_t t256_lists = 2 * std::max<int64_t>(1, 512 / cdiv(B, 128));  // (split, row half) lists of t256 / kb256
   const int64_t p_need = (int64_t)B *
                          std::max<int64_t>(std::max(std::max(max_splits, wide_splits), t256_lists), kSampleMax / kTileRows) *
                          k;
@@ -3439,10 +3389,10 @@ int ensure_query_ws(ahr_index* ix, int B, int k, hipStream_t s) {
     if (ix->part) AHR_HIP(hipFree(ix->part));
     ix->part = nullptr;
     ix->part_cap = 0;
-    if (hipMalloc(&ix->part, (p_need + 8 + 128) * sizeof(uint64_t)) != hipSuccess)
+    if (hipMalloc(&ix->part, (p_need + 8) * sizeof(uint64_t)) != hipSuccess)
       return fail(AHR_ENOMEM, "partial top-k workspace allocation failed");
     ix->part_cap = p_need;
-    AHR_HIP(hipMemsetAsync(ix->part + p_need, 0, (8 + 128) * sizeof(uint64_t), s));  // fold counter, kb pace
+    AHR_HIP(hipMemsetAsync(ix->part + p_need, 0, 8 * sizeof(uint64_t), s));  // the small kernels' fold counter
   }
   const int64_t s_need = (int64_t)B * (kGroupMax + 1);
   if (s_need > ix->sample_cap) {
@@ -3501,7 +3451,7 @@ void launch_tilelane(const ahr_index* ix, const SearchPlan& p, int n_rows, int B
 // lane's private list inside the kernel, so the cap only trades memory for speed.
 inline int qkv_cand_cap(const SearchPlan& p) { return (int)std::min(64, std::max(16, p.tiles_per_split)); }
 inline int64_t cand_bytes(int B, const SearchPlan& p) {
-  const int64_t prod = (p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256 || p.kernel == KERNEL_KB128) ? 8 : 4;  // producers per (query, split)
+  const int64_t prod = (p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) ? 8 : 4;  // producers per (query, split)
   return (int64_t)B * prod * p.n_splits * qkv_cand_cap(p) * 8;
 }
 
@@ -3538,18 +3488,6 @@ void launch_t256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, in
                      thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
 
-// kb256 split pacing lead in k-steps (AHR_KB_PACE_LEAD; default 0 = off). Measured at C3 (5M x
-// 768 f16, B = 1024, one box, alternating): lead 12 cuts the bytes beyond L2 from 13.5 to 10.6 GB
-// per launch (1.76x -> 1.38x of the corpus) but costs 4-5 % (7.71-7.80 -> 8.09-8.10 ms): the
-// kernel is bound by its MFMA/DMA-issue core, not by HBM, and pacing adds waits.
-inline int kb_pace_lead() {
-  static const int lead = [] {
-    const char* e = getenv("AHR_KB_PACE_LEAD");
-    return e ? atoi(e) : 0;
-  }();
-  return lead;
-}
-
 template <int DT, int KCAP, int WN>
 void launch_kb256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, int k, uint32_t row_base,
                   const float* thr, int flags, hipStream_t s) {
@@ -3559,8 +3497,7 @@ void launch_kb256(const ahr_index* ix, const SearchPlan& p, int n_rows, int B, i
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), C::kLds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_splits * p.qblocks)), dim3(C::kThreads), C::kLds, s, ix->rows_kb,
                      ix->qbuf_kb, ix->d_pad * ix->elem / kb256::kKB, n_rows, B, p.n_row_tiles, row_base, k, ix->part,
-                     thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p),
-                     ix->kb_pace(), ++ix->kb_epoch, kb_pace_lead());
+                     thr, p.n_splits, p.qblocks, flags, reinterpret_cast<uint64_t*>(ix->cand), qkv_cand_cap(p));
 }
 
 template <int DT, int NKT>
@@ -3664,18 +3601,17 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     if (p.kernel == KERNEL_SMALL) {
       prof_mark(ix, 2, s);
       const float* qs = small_fuses_convert(ix) ? q : nullptr;
-      switch (small::groups(B)) {
-        case 1: launch_small_k<DT, 1>(ix, p, qs, normalize_q, B, k, row_base, fold, s); break;
-        case 2: launch_small_k<DT, 2>(ix, p, qs, normalize_q, B, k, row_base, fold, s); break;
-        default: launch_small_k<DT, 4>(ix, p, qs, normalize_q, B, k, row_base, fold, s); break;
-      }
+      launch_small_k<DT, 1>(ix, p, qs, normalize_q, B, k, row_base, fold, s);
       return;
     }
   }
   const int S = sample_rows_for(ix);
+  // the register-resident kernel seeds itself (no pre-pass launch) unless kFlagQresPrepass asks for
+  // the sampled pre-pass (A/B) or the caller supplies seeds
+  const bool self_seed = p.kernel == KERNEL_QRES && S > 0 && !ix->seed && !(ix->debug_flags & kFlagQresPrepass);
   if (ix->seed) {
     thr = ix->seed;  // the caller's valid lower bounds of each query's k-th best score
-  } else if (S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
+  } else if (!self_seed && S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
     // Threshold pre-pass: score the first S rows, take each query's k-th best.
     float* scores = ix->sample;
     float* t = ix->sample + (int64_t)B * (S / 16);
@@ -3687,11 +3623,17 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   }
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
-  const int flags = (p.xcd_remap ? kFlagXcdRemap : 0) | ix->debug_flags;
+  const uint32_t flags = (p.xcd_remap ? kFlagXcdRemap : 0u) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
     if (p.kernel == KERNEL_QRES) {
-      qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, n, B, row_base, ix->part, thr, p.n_splits,
-                   p.qblocks, flags, s);
+      uint64_t* pub = nullptr;
+      uint64_t* seeds = nullptr;
+      if (self_seed) {  // tag, [q_cap][n_splits] maxima, [q_cap] seeds
+        pub = ix->ss + 1;
+        seeds = pub + ix->q_cap * (int64_t)p.n_splits;
+      }
+      qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
+                   p.n_splits, p.qblocks, (int)flags, pub, seeds, reinterpret_cast<const uint32_t*>(ix->ss), s);
       return;
     }
     if (p.kernel == KERNEL_KB256) {
@@ -3701,15 +3643,6 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
         launch_kb256<DT, 12, 4>(ix, p, n, B, k, row_base, thr, flags, s);
       else
         launch_kb256<DT, 16, 4>(ix, p, n, B, k, row_base, thr, flags, s);
-      return;
-    }
-    if (p.kernel == KERNEL_KB128) {
-      if (k <= 8)
-        launch_kb256<DT, 8, 2>(ix, p, n, B, k, row_base, thr, flags, s);
-      else if (k <= 12)
-        launch_kb256<DT, 12, 2>(ix, p, n, B, k, row_base, thr, flags, s);
-      else
-        launch_kb256<DT, 16, 2>(ix, p, n, B, k, row_base, thr, flags, s);
       return;
     }
     if (p.kernel == KERNEL_T256) {
@@ -3728,10 +3661,6 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
         launch_qkv_k<DT, 6>(ix, p, n, B, k, row_base, thr, flags, s);
       return;
     }
-  }
-  if (p.kernel == KERNEL_LANE256Q128) {
-    launch_lane_k<DT, 8, 1, 1, 4, 2, 2>(ix, p, n, B, k, row_base, thr, flags, s);
-    return;
   }
   if (p.kernel == KERNEL_TILELANE) {
     switch (k <= 8 ? 8 : (k <= 12 ? 12 : 16)) {  // lists sized to k
@@ -3846,15 +3775,11 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   // the register-resident plan's fragment-major query copy (qbuf_kb: the k-blocked copy's buffer)
   bool frag_done = false;
   if (pre_kernel == KERNEL_QRES) {
-    if (!ix->qbuf_kb) {
-      if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
-        return fail(AHR_ENOMEM, "query workspace allocation failed");
-      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
-    }
+    if ((st = ensure_qbuf_kb(ix, s)) || (st = ensure_ss(ix, s))) return st;
     if (small_fuses_convert(ix)) {  // one launch: rows + fragments
       hipLaunchKernelGGL(convert_queries_frag_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B,
                          ix->dim, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, ix->dtype, ix->qbuf_kb,
-                         qres::frag_mode(k, ix->debug_flags));
+                         reinterpret_cast<uint32_t*>(ix->ss));
       frag_done = true;
     }
   }
@@ -3863,7 +3788,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
                        (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                        ix->row_stride, ix->d_pad, ix->dtype);
   if (pre_kernel == KERNEL_QRES && !frag_done)
-    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, k, ix->qbuf_kb, ix->debug_flags, s);
+    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, ix->qbuf_kb, reinterpret_cast<uint32_t*>(ix->ss), s);
   if (k > AHR_MAX_K) {
     switch (ix->dtype) {
       case AHR_BF16: return run_query_large_k<DT_BF16>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);
@@ -3872,7 +3797,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     }
   }
   SearchPlan p = plan_search(ix, B, k);
-  const bool kb_plan = p.kernel == KERNEL_KB256 || p.kernel == KERNEL_KB128;
+  const bool kb_plan = p.kernel == KERNEL_KB256;
   const bool cand_plan = p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || kb_plan;
   if (cand_plan && ix->count > 0) {
     st = ensure_cand(ix, cand_bytes(B, p));
@@ -3890,11 +3815,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
       hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(all, 256)), dim3(256), 0, s, ix->rows,
                          ix->row_stride, (int64_t)0, ix->count, n_kb, ix->rows_kb);
     }
-    if (!ix->qbuf_kb) {
-      if (hipMalloc(&ix->qbuf_kb, ix->q_cap * ix->row_stride) != hipSuccess)
-        return fail(AHR_ENOMEM, "query workspace allocation failed");
-      AHR_HIP(hipMemsetAsync(ix->qbuf_kb, 0, ix->q_cap * ix->row_stride, s));
-    }
+    if ((st = ensure_qbuf_kb(ix, s))) return st;
     const int64_t chunks = (int64_t)B * n_kb * 4;
     hipLaunchKernelGGL(reblock_kb_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0, s, ix->qbuf,
                        ix->row_stride, (int64_t)0, (int64_t)B, n_kb, ix->qbuf_kb);
@@ -3973,6 +3894,7 @@ int ahr_index_destroy(ahr_index* ix) {
   if (ix->part) (void)hipFree(ix->part);
   if (ix->sample) (void)hipFree(ix->sample);
   if (ix->cand) (void)hipFree(ix->cand);
+  if (ix->ss) (void)hipFree(ix->ss);
   for (int w = 0; w < kMaxWorkspaces; ++w) {
     if (w == ix->cur_ws) continue;
     if (ix->parked[w].qbuf) (void)hipFree(ix->parked[w].qbuf);
@@ -3980,6 +3902,7 @@ int ahr_index_destroy(ahr_index* ix) {
     if (ix->parked[w].part) (void)hipFree(ix->parked[w].part);
     if (ix->parked[w].sample) (void)hipFree(ix->parked[w].sample);
     if (ix->parked[w].cand) (void)hipFree(ix->parked[w].cand);
+    if (ix->parked[w].ss) (void)hipFree(ix->parked[w].ss);
   }
   for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
   delete ix;
@@ -4142,20 +4065,16 @@ int ahr_index_set_seed(ahr_index* ix, const float* thr) {
   return AHR_OK;
 }
 
-int ahr_index_set_debug_flags(ahr_index* ix, int flags) {
+int ahr_index_set_debug_flags(ahr_index* ix, uint32_t flags) {
   if (!ix) return fail(AHR_EINVAL, "null index");
+  if (flags & ~(kKnownFlags | kFlagXcdRemap)) return fail(AHR_EINVAL, "unknown debug flag bits");
   // The cost-split switches give wrong results by design; only the ablation build
   // (__graft_entry__.build_ablation, -DAHR_ABLATION) accepts them, the shipped library refuses.
-  constexpr int kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
-                                    kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead;
 #ifndef AHR_ABLATION
   if (flags & kWrongResultFlags)
     return fail(AHR_EUNSUP, "result-corrupting ablation flags need the AHR_ABLATION build");
 #endif
-  ix->debug_flags = flags & (kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagNoTilePrefetch |
-                             kKernelFlags | kFlagSmallWide | kFlagTileZero | kFlagTileFirst | kFlagNoFold |
-                             kFlagNoBarrier | kFlagNoLdsRead | kFlagQresStagger | kFlagQresScreenLoop |
-                             kFlagQres16 | kFlagQres4w | kFlagKbNoPace | kFlagQresBlkSync);
+  ix->debug_flags = flags & kKnownFlags;
   return AHR_OK;
 }
 
@@ -4173,6 +4092,8 @@ int ahr_index_set_workspace(ahr_index* ix, int slot) {
   out.sample_cap = ix->sample_cap;
   out.cand = ix->cand;
   out.cand_cap = ix->cand_cap;
+  out.ss = ix->ss;
+  out.ss_cap = ix->ss_cap;
   ahr_query_ws& in = ix->parked[slot];
   ix->qbuf = in.qbuf;
   ix->qbuf_kb = in.qbuf_kb;
@@ -4183,6 +4104,8 @@ int ahr_index_set_workspace(ahr_index* ix, int slot) {
   ix->sample_cap = in.sample_cap;
   ix->cand = in.cand;
   ix->cand_cap = in.cand_cap;
+  ix->ss = in.ss;
+  ix->ss_cap = in.ss_cap;
   in = ahr_query_ws{};
   ix->cur_ws = slot;
   return AHR_OK;
@@ -4205,12 +4128,19 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k) {
   DeviceGuard dg(ix->device);
   int st = ensure_query_ws(ix, max_batch, max_k, nullptr);
   if (st) return st;
-  // candidate groups of the query-resident plan at the current corpus size
+  // the plan-specific buffers at the current corpus size: candidate groups (qkv, t256, kb256), the
+  // second query buffer (kb256, qres256) and the self-seeding granules (qres256)
   for (int kk = 1; kk <= max_k; kk = kk < 8 ? 8 : kk + 8) {
     const SearchPlan p = plan_search(ix, max_batch, kk);
-    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256 || p.kernel == KERNEL_KB128) {
+    if (p.kernel == KERNEL_QKV || p.kernel == KERNEL_T256 || p.kernel == KERNEL_KB256) {
       st = ensure_cand(ix, cand_bytes(max_batch, p));
       if (st) return st;
+    }
+    if (p.kernel == KERNEL_KB256 || p.kernel == KERNEL_QRES) {
+      if ((st = ensure_qbuf_kb(ix, nullptr))) return st;
+    }
+    if (p.kernel == KERNEL_QRES) {
+      if ((st = ensure_ss(ix, nullptr))) return st;
     }
   }
   AHR_HIP(hipDeviceSynchronize());  // zeroing done before any stream uses the workspace

@@ -121,6 +121,14 @@ __device__ __forceinline__ void blds16_soff(__amdgpu_buffer_rsrc_t r, uint32_t v
                                            0);
 }
 
+// The register-resident plan's self-seeding tag: the query conversion before each launch advances
+// it on the device (one thread), so every launch — a replayed hipGraph's too — gets its own; 0 is
+// never used (zeroed granule buffers hold tag 0).
+__device__ __forceinline__ void advance_epoch(uint32_t* e) {
+  const uint32_t v = *e + 1u;
+  *e = v ? v : 1u;
+}
+
 // Workgroup barrier that waits for this wave's LDS traffic but leaves global_load_lds in flight
 // (__syncthreads() would emit vmcnt(0) and drain the ring).
 __device__ __forceinline__ void lds_barrier() {
@@ -163,12 +171,12 @@ __device__ __forceinline__ uint64_t list_at(const uint64_t (&L)[KCAP], int idx) 
 }
 
 enum { MODE_TOPK = 0, MODE_GROUPMAX = 1, MODE_SCORES = 2 };
-enum {
+// Plan / ablation flag bits: a uint32_t word (ahr_index_set_debug_flags).
+enum : uint32_t {
   kFlagXcdRemap = 1,
   kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
   kFlagTile128 = 8,       // the 128x128 tile kernel with cooperative screening, any k
   kFlagTileLane = 32,     // the 128x128 lane-local kernel at any batch (k <= 16)
-  kFlagLane256q128 = 64,  // lane kernel with 256 rows x 128 queries, 2 workgroups / CU
   kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
   kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
   kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
@@ -176,32 +184,31 @@ enum {
   kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
   kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
   kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagSmallWide = 65536,  // the small-batch kernel up to B = 64 (2 or 4 query groups; measured slower)
   kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagNoKB256 = 262144,  // plan without the k-blocked kernels
-  kFlagKB128 = 524288,    // the k-blocked 256x128 kernel wherever it applies (bf16/f16, k <= 16)
-  kFlagTileZero = 1 << 20,   // k-blocked kernels: every tile's operands read from tile 0 (L2-resident; wrong results)
-  kFlagTileFirst = 1 << 21,  // k-blocked kernels: every tile read from the split's first tile (wrong results)
-  kFlagNoFold = 1 << 22,     // small kernels: merge launch instead of the last-workgroup fold (A/B)
-  kFlagQres = 1 << 23,       // the 256-query register-resident kernel wherever it applies (bf16/f16, d 768, k <= 12)
-  kFlagNoBarrier = 1 << 24,  // qres kernel: no stage barriers (wrong results)
-  kFlagNoLdsRead = 1 << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
-  kFlagQresStagger = 1 << 26,     // qres kernel: waves 4-7 one stage behind waves 0-3 (A/B; same results)
-  kFlagQresScreenLoop = 1 << 27,  // qres kernel: pass-mask + select-chain screening (A/B; same results)
-  kFlagQres16 = 1 << 28,          // qres: the 16x16x32 form (k <= 10; A/B)
-  kFlagQres4w = 1 << 29,          // qres: the 16x16x32 form with 4 waves of 64 queries, 1 per SIMD (k <= 10; A/B)
-  kFlagKbNoPace = 1 << 30,        // kb256: no split pacing (A/B; same results)
-  kFlagQresBlkSync = 1 << 31,         // qres (32x32x16 form): one barrier per block instead of per stage (A/B)
+  kFlagNoKB256 = 262144,  // plan without the k-blocked kernel
+  kFlagTileZero = 1u << 20,   // k-blocked kernel: every tile's operands read from tile 0 (L2-resident; wrong results)
+  kFlagTileFirst = 1u << 21,  // k-blocked kernel: every tile read from the split's first tile (wrong results)
+  kFlagNoFold = 1u << 22,     // small kernels: merge launch instead of the last-workgroup fold (A/B)
+  kFlagQres = 1u << 23,       // the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 12)
+  kFlagNoBarrier = 1u << 24,  // qres kernel: no stage barriers (wrong results)
+  kFlagNoLdsRead = 1u << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
+  kFlagQresPrepass = 1u << 26,   // qres kernel seeded by the sampled pre-pass launch, not by itself (A/B)
+  kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first round only (A/B)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
 #else
 constexpr bool kAblation = false;
 #endif
-constexpr int kKernelFlags = kFlagTile128 | kFlagTileLane | kFlagLane256q128 | kFlagNoQres | kFlagQkv | kFlagT256 |
-                             kFlagKB256 | kFlagNoKB256 | kFlagKB128 | kFlagQres;
+constexpr uint32_t kKernelFlags =
+    kFlagTile128 | kFlagTileLane | kFlagNoQres | kFlagQkv | kFlagT256 | kFlagKB256 | kFlagNoKB256 | kFlagQres;
 // the flags that request a kernel (the kFlagNo* ones only take one out of the plan)
-constexpr int kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
+constexpr uint32_t kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
+// every flag ahr_index_set_debug_flags accepts; those that give wrong results need the ablation build
+constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
+                                       kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead;
+constexpr uint32_t kKnownFlags = kKernelFlags | kWrongResultFlags | kFlagNoTilePrefetch | kFlagNoFold |
+                                 kFlagQresPrepass | kFlagQresSeedOnce;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 }  // namespace dense

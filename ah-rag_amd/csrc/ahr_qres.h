@@ -13,26 +13,25 @@ constexpr int kTQ = 256;     // queries per workgroup: 8 waves x 32
 constexpr int kTR = 32;      // corpus rows per block
 constexpr int kBufCap = 16;  // per-lane survivor buffer (keys) in LDS
 
-// bf16 / f16 rows of d_pad_bytes = 1536 (d_pad = 768), k <= 12: what the kernel is built for.
+// bf16 / f16 rows of d_pad_bytes = 1536 or 768 (d_pad = 768 or 384), k <= 12: what the kernel is built for.
 bool supported(int dtype, int d_pad_bytes, int k);
 
 // Query rows [B][row_stride] (the convert kernel's storage rows) -> the fragment-major copy the
-// planned form reads, one contiguous KiB per wave B operand: 16x16x32 form [B/16 groups][d_pad/32
-// k32 steps][64 lanes][16 B] (lane l: query 16g + l%16, bytes [64 S + 16 (l/16), +16)); 32x32x16
-// form [B/32][d_pad/16 k16 steps][64][16 B] (lane l: query 32g + l%32, bytes [32 S + 16 (l/32), +16)).
-// The buffers are padded to whole 256-query blocks.
-void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes, int k, uint8_t* qfrag, int flags,
+// kernel reads, one contiguous KiB per wave B operand: [B/32][d_pad/16 k16 steps][64 lanes][16 B]
+// (lane l: query 32g + l%32, bytes [32 S + 16 (l/32), +16)). The buffer is padded to whole
+// 256-query blocks.
+// epoch (optional): the self-seeding tag this launch advances (see launch).
+void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes, uint8_t* qfrag, uint32_t* epoch,
                  hipStream_t s);
-
-// The fragment layout the planned form reads: 16 (16x16x32 form) or 32 (32x32x16 form), for the
-// fused conversion (convert_queries_frag_kernel) that writes it directly.
-int frag_mode(int k, int flags);
 
 // One fused launch: part_keys [B][n_splits][k] (the merge kernels' input), thr [B] optional
 // admission seeds. grid = n_splits * qblocks; n_splits % 8 == 0 when flags has the XCD remap bit.
-void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
-            uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
-            hipStream_t s);
+// pub [q_pad][n_splits] / seeds [q_pad] (q_pad = 256 * qblocks rounded up to the workspace): the
+// self-seeding granules, nullptr for none; *epoch: the launch's tag, which the query conversion
+// stream-ordered before this launch advanced (no earlier launch on these buffers used it).
+void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int d_pad_bytes,
+            int n_rows, int B, uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks,
+            int flags, uint64_t* pub, uint64_t* seeds, const uint32_t* epoch, hipStream_t s);
 
 }  // namespace qres
 }  // namespace dense

@@ -6,28 +6,39 @@
 // at C2 that is ~8.6 MB per CU per launch, which the per-CU L2 -> LDS delivery (~69 GB/s
 // measured) cannot feed faster than ~124 us (the GEMM-only time of topk_tilelane_kernel). Here
 // a workgroup keeps 256 queries resident in VGPRs for the whole launch — wave w holds the B
-// fragments of queries 32w .. 32w + 31 over the WHOLE dimension (48 x 16 B per lane at
-// d = 768, 192 VGPRs) — and only the corpus streams: 1 byte per 256 flops, 4x fewer than the
-// tile kernels. Every wave multiplies every 32-row corpus block (the A operand, read from LDS)
-// against its own queries with one v_mfma_f32_32x32x16 chain per block (48 steps), so a corpus
+// fragments of queries 32w .. 32w + 31 over the WHOLE dimension (NKT * 4 x 16 B per lane: 192
+// VGPRs at d = 768, 96 at d = 384) — and only the corpus streams: 1 byte per 256 flops, 4x fewer
+// than the tile kernels. Every wave multiplies every 32-row corpus block (the A operand, read
+// from LDS) against its own queries with one v_mfma_f32_32x32x16 chain per block, so a corpus
 // byte brought in is used by 8 waves.
 //
-// * Corpus: 32-row blocks, each split into two stages of 6 k-tiles (64-deep, 128 B per row:
-//   24 KiB); a 4-slot ring filled by buffer LDS-DMA three stages ahead (1-KiB pieces of 8 whole
-//   128-B rows, 3 per wave per stage), the XOR chunk swizzle of the tile kernels (conflict-free
-//   ds_read_b128). One barrier per stage.
+// * Corpus: 32-row blocks in stages of 6 k-tiles (64-deep, 128 B per row: 24 KiB; 2 stages per
+//   block at d_pad = 768, 1 at 384); a 4-slot ring filled by buffer LDS-DMA two stages ahead
+//   (1-KiB pieces of 8 whole 128-B rows, 3 per wave per stage), the XOR chunk swizzle of the tile
+//   kernels (conflict-free ds_read_b128). One barrier per stage.
 // * Scores: the k-order, fragment map and accumulation chain of topk_tilelane_kernel (step s of
 //   a row covers k = [16 s, 16 s + 16), lane half fh holding 8 of them; the chain starts from 0),
 //   so every score is bitwise the tile kernel's.
 // * Top-k: a lane holds one query column x 16 rows of each block. Its 16 scores are screened
-//   against the lane's threshold (the pre-pass seed, then the lane's own k-th best): the block
-//   max in the common case, and for the rare passing scores one 8-B append to the lane's
-//   16-entry LDS buffer. A full buffer is compacted in place to its k best, which raises the
-//   threshold. At the end each lane sorts its buffer into a register list (the query registers
-//   are dead by then) and the two lanes of a query merge: one list per (query, split).
+//   against the lane's threshold: the block max in the common case, and for the rare passing
+//   scores one 8-B append to the lane's 16-entry LDS buffer. A full buffer is compacted in place
+//   to its k best, which raises the threshold. At the end each lane sorts its buffer into a
+//   register list (the query registers are dead by then) and the two lanes of a query merge:
+//   one list per (query, split).
+// * Admission threshold, self-seeded (no pre-pass launch): the 64 splits of a query block share
+//   a rising lower bound of each query's k-th best score through memory. A split publishes, per
+//   query, the max score of the rows it has scored so far (one 8-B {epoch, ord(score)} granule,
+//   write-through); the split that owns query j (j mod n_splits) takes the k-th largest of the
+//   published maxima — k distinct rows score at least that much, so it is a valid lower bound of
+//   the k-th best — and publishes it as the query's seed, which every split reads. First round:
+//   maxima of each split's first block (a 2,048-row sample at C2), the block's raw scores parked
+//   in the lane buffer meanwhile and screened against the seed once it is there (a short bounded
+//   wait at the end of block 1); later rounds (maxima over 4, 8, 16, ... blocks) tighten it
+//   without waiting. Granules carry the launch's epoch, so a stale or absent one only weakens
+//   the seed, never invalidates it; every wait is bounded, so nothing assumes co-residency.
 // * Query fragments come from a fragment-major copy of the converted queries (launch_frag):
 //   one coalesced 1-KiB load per wave per k16 step.
-// * Budget: 192 query VGPRs + 16 accumulators + fragments in flight <= 256 (two waves per SIMD,
+// * Budget: NKT*16 query VGPRs + 16 accumulators + fragments in flight <= 256 (two waves per SIMD,
 //   one workgroup of 8 waves per CU); LDS 96 KiB ring + 64 KiB lane buffers = 160 KiB.
 #include "ahr_qres_common.h"
 
@@ -35,26 +46,89 @@ namespace ahr {
 namespace dense {
 namespace qres {
 
-
 template <int NKT>
 struct Cfg {
-  static_assert(NKT % 2 == 0, "two stages per block");
-  static constexpr int kSK = NKT / 2;          // k-tiles per stage
-  static constexpr int kStage = kSK * kKt;     // 24 KiB at d_pad = 768
-  static constexpr int kPieces = kSK * 4;      // 1-KiB DMA pieces per stage (8 rows x 128 B)
+  static_assert(NKT % 6 == 0, "stages of 6 k-tiles");
+  static constexpr int kSK = 6;                   // k-tiles per stage
+  static constexpr int kSPB = NKT / kSK;          // stages per 32-row block
+  static constexpr int kStage = kSK * kKt;        // 24 KiB
+  static constexpr int kPieces = kSK * 4;         // 1-KiB DMA pieces per stage (8 rows x 128 B)
   static_assert(kPieces % kWaves == 0, "equal DMA share per wave");
-  static constexpr int kPPW = kPieces / kWaves;  // pieces per wave per stage
-  static constexpr int kNS = NKT * 4;          // k16 steps = query fragments per lane
-  static constexpr int kSS = kSK * 4;          // k16 steps per stage
-  static constexpr int kOffBuf = kSlots * kStage;
+  static constexpr int kPPW = kPieces / kWaves;   // pieces per wave per stage
+  static constexpr int kNS = NKT * 4;             // k16 steps = query fragments per lane
+  static constexpr int kSS = kSK * 4;             // k16 steps per stage
+  // LDS: the ring, the seeding scratch (per wave 3 KiB: the tail of the first seed's parked
+  // accumulators, a round's selection granules, a round's seed granules), the lane buffers
+  static constexpr int kOffSeed = kSlots * kStage;
+  static constexpr int kSeedBytes = kWaves * 3 * 1024;
+  static constexpr int kOffBuf = kOffSeed + kSeedBytes;
   static constexpr int kLds = kOffBuf + kBufCap * kThreads * 8;
 };
 static_assert(Cfg<12>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
 
+// Self-seeding schedule over a split's block index bi (uniform): publish the running maxima after
+// block 0, 3, 7, 15, ...; the first seed is selected and read at the end of block 1 (bounded
+// waits); later rounds select D blocks after their publication and read D blocks after that (D =
+// 1 at two stages per block, 2 at one: the granules travel by LDS-DMA issued one stage ahead).
+__device__ __forceinline__ bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
+__device__ __forceinline__ bool ss_pub(int bi) { return bi == 0 || (bi >= 3 && pow2(bi + 1)); }
+__device__ __forceinline__ bool ss_round(int bi) { return bi >= 3 && pow2(bi + 1); }
+constexpr uint32_t kSeedWaitTicks = 3000;  // s_memrealtime ticks (100 MHz): a 30-us bound per wait
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, false);
+}
+// wave64 max of u32 values (the DPP sequence of wave_max_u64), in every lane
+__device__ __forceinline__ uint32_t dpp_max_u32(uint32_t x) {
+  x = max(x, dpp_u32<0x111, 0xf>(x));  // row_shr:1
+  x = max(x, dpp_u32<0x112, 0xf>(x));  // row_shr:2
+  x = max(x, dpp_u32<0x114, 0xf>(x));  // row_shr:4
+  x = max(x, dpp_u32<0x118, 0xf>(x));  // row_shr:8
+  x = max(x, dpp_u32<0x142, 0xa>(x));  // row_bcast:15
+  x = max(x, dpp_u32<0x143, 0xc>(x));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// k-th largest of the wave's nonzero values (lane l holds v0, v1); 0 if fewer than k are nonzero.
+// k rounds of a wave max, each removing one instance (the lowest lane holding it).
+__device__ __forceinline__ uint32_t wave_kth(uint32_t v0, uint32_t v1, int k, int lane) {
+  uint32_t m = 0;
+#pragma unroll 1
+  for (int r = 0; r < k; ++r) {
+    const uint32_t lm = max(v0, v1);
+    m = dpp_max_u32(lm);
+    if (m == 0) return 0;
+    const int first = __builtin_ctzll(__ballot(lm == m));
+    if (lane == first) {
+      if (v0 == m)
+        v0 = 0;
+      else
+        v1 = 0;
+    }
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint64_t granule_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: not from L1
+}
+__device__ __forceinline__ void granule_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
+}
+// 1 KiB of granules (64 lanes x 16 B from base; bytes past `bytes` read as 0) into LDS by an sc1
+// LDS-DMA: no registers held while it is in flight, and it retires in order with the ring's DMA
+__device__ __forceinline__ void granules_to_lds(const uint64_t* base, uint32_t bytes, unsigned char* lds, int lane) {
+  const __amdgpu_buffer_rsrc_t r = tile_rsrc_u(base, bytes);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (uint32_t)lane * 16,
+                                           0, 0, 16 /* sc1 */);
+}
+
 
 __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ qbuf, int64_t row_stride, int64_t n16,
-                                                   int ns, uint8_t* __restrict__ qfrag) {
+                                                   int ns, uint8_t* __restrict__ qfrag, uint32_t* __restrict__ epoch) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 16-B chunk of the output
+  if (i == 0 && epoch) advance_epoch(epoch);
   if (i >= n16) return;
   const int l = (int)(i & 63);
   const int64_t gs = i >> 6;
@@ -65,13 +139,16 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
 }
 
 
-// SYNC: 0 = a workgroup barrier per stage (default), 1 = the same with waves 4-7 one stage
-// behind (A/B), 2 = one barrier per block (A/B).
-template <int DT, int NKT, int KCAP, int SYNC, int SCR, int ABL>
+// pub [q_pad][n_splits] and seeds [q_pad]: the self-seeding granules (nullptr: no self-seeding;
+// thr_init, if any, is the admission threshold). *epoch_p: this launch's tag, advanced on the
+// device by the query conversion launched before it (so a replayed hipGraph gets a fresh one).
+// ROUNDS: the later self-seeding rounds compiled in (the first round is always there).
+template <int DT, int NKT, int KCAP, int ABL, bool ROUNDS>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
-    int qblocks, int flags) {
+    int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t* __restrict__ seeds,
+    const uint32_t* __restrict__ epoch_p) {
   using C = Cfg<NKT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -94,32 +171,40 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // control flow built on them scalar)
   const int b_begin = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n_blocks / n_splits));
   const int b_end = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n_blocks / n_splits));
-  const int n_st = 2 * (b_end - b_begin);
+  const int n_st = C::kSPB * (b_end - b_begin);
   const int qw0 = qb * kTQ + wave * 32;
   const bool live = qw0 < n_q;  // wave-uniform: a wave past the batch only stages and syncs
   const int q = qw0 + fr;
+  // self-seeding needs every split's first two blocks and at most 128 splits (grid-uniform)
+  const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && n_blocks >= 2 * n_splits && n_splits <= 128;
+  // later rounds: at most one selected query per wave (n_splits >= 32)
+  const bool ss_rounds = ROUNDS && ss && n_splits >= 32;
+  constexpr int kD = C::kSPB == 1 ? 2 : 1;  // blocks from a round's publication to its selection
 
   float thr = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+  const uint32_t epoch = pub ? *epoch_p : 0u;
 
   // DMA: piece p = wave + 8 i of a stage is k-tile p / 4, rows 8 (p % 4) .. +8; lane l lands at
   // (row 8 (p % 4) + l / 8, physical chunk l % 8) and loads logical chunk (l % 8) ^ swz(row)
-  uint32_t src_off[C::kPPW];
-  int dst_off[C::kPPW];
-#pragma unroll
-  for (int i = 0; i < C::kPPW; ++i) {
-    const int p = wave + kWaves * i;
-    const int row = 8 * (p & 3) + (lane >> 3);
-    src_off[i] = (uint32_t)(row * row_stride) + (p >> 2) * kRowBytes + ((((lane & 7) ^ ((row >> 1) & 7))) << 4);
-    dst_off[i] = (p >> 2) * kKt + (p & 3) * 1024;
-  }
+  // (the per-lane source offsets are recomputed at each issue: a few VALU per stage, and three
+  // registers the main loop cannot spare)
   const uint32_t blk_bytes = (uint32_t)(kTR * row_stride);
+  auto slot_of = [&](int st) __attribute__((always_inline)) { return smem + (st % kSlots) * C::kStage; };
   auto issue = [&](int st) __attribute__((always_inline)) {
-    const int b = b_begin + (st >> 1);
+    const int b = b_begin + st / C::kSPB;
     const __amdgpu_buffer_rsrc_t r =
-        tile_rsrc(corpus + (int64_t)b * kTR * row_stride + (st & 1) * C::kSK * kRowBytes, blk_bytes);
-    unsigned char* slot = smem + (st & (kSlots - 1)) * C::kStage;
+        tile_rsrc(corpus + (int64_t)b * kTR * row_stride + (st % C::kSPB) * C::kSK * kRowBytes, blk_bytes);
+    unsigned char* slot = slot_of(st);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
 #pragma unroll
-    for (int i = 0; i < C::kPPW; ++i) blds16(r, src_off[i], slot + dst_off[i]);
+    for (int i = 0; i < C::kPPW; ++i) {
+      const int p = wave + kWaves * i;
+      const int row = 8 * (p & 3) + (ln >> 3);
+      const uint32_t src_off =
+          (uint32_t)(row * row_stride) + (p >> 2) * kRowBytes + ((((ln & 7) ^ ((row >> 1) & 7))) << 4);
+      blds16(r, src_off, slot + (p >> 2) * kKt + (p & 3) * 1024);
+    }
   };
   if (n_st > 0) issue(0);
   if (n_st > 1) issue(1);
@@ -137,13 +222,23 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 #pragma unroll
   for (int S = 0; S < C::kNS; ++S) asm volatile("" : "+v"(qf[S]));
   asm volatile("" : "+v"(thr));
-  uint64_t thk = (q < n_q && thr != -INFINITY) ? (((uint64_t)ord_f32(thr) << 32) - 1) : 0;
+  // (a score threshold only, no key: a score equal to it always passes, so exact ties may be
+  // appended and cut again — correct, and the registers go to the resident fragments)
 
   // lane survivor buffer: entry c at lbuf[c * kThreads] (a wave's 64 lanes hit 64 consecutive u64)
-  uint64_t* lbuf = reinterpret_cast<uint64_t*>(smem + C::kOffBuf) + tid;
+  uint64_t* const lbuf0 = reinterpret_cast<uint64_t*>(smem + C::kOffBuf);
+  auto lb = [&]() __attribute__((always_inline)) {  // recomputed at each use: not a live register
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    return lbuf0 + t;
+  };
+  // this wave's seeding scratch: [0, 1 KiB) parked accumulator tail, [1, 2) selection granules,
+  // [2, 3) seed granules
+  unsigned char* const wscr = smem + C::kOffSeed + wave * 3 * 1024;
   int nb = 0;
   // keep the k_out best buffered keys; the smallest kept is the lane's k-th best: new threshold
   auto compact = [&]() {
+    uint64_t* const lbuf = lb();
 #pragma unroll 1
     while (nb > k_out) {
       int mi = 0;
@@ -165,102 +260,166 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       const uint64_t v = lbuf[c * kThreads];
       mn = v < mn ? v : mn;
     }
-    if (mn > thk) {
-      thk = mn;
-      thr = key_score(mn);
+    thr = fmaxf(thr, key_score(mn));
+  };
+  // the rows of score e of quad qd: r0 + 8 qd + 4 fh + e. A passing quad's scores are tested one by
+  // one, each passing score one append; a quad compacts first when its 4 possible appends might
+  // not fit.
+  auto screen_quad = [&](float v0, float v1, float v2, float v3, int qrow, bool ragged) __attribute__((always_inline)) {
+    if (nb + 4 > kBufCap) compact();
+    uint64_t* const lbuf = lb();
+    const float vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t row = (uint32_t)(qrow + e);
+      if (vv[e] >= thr && (!ragged || row < (uint32_t)n_rows)) {
+        if (nb == kBufCap) compact();  // k_out + 4 > kBufCap (k = 12): one more cut mid-quad
+        lbuf[nb * kThreads] = make_key(vv[e], row_base + row);
+        ++nb;
+      }
     }
   };
-  // a block's 16 scores of this lane: rows r0 + 8 (j / 4) + 4 fh + j % 4.
-  // SCR = 1 (default): quad maxima (the 4 rows of a register quad), then exec-masked tests of the
-  // passing quads' scores, each passing score one append; a quad compacts first when its 4
-  // possible appends might not fit. SCR = 0: a pass mask and a select chain per passing score.
+  float rm = -INFINITY;  // self-seeding: max score of this lane's rows so far
+  // a block's 16 scores of this lane: quad maxima, then the passing quads
   auto screen_quads = [&](const f32x16& acc, int r0) __attribute__((always_inline)) {
     float qm[4];
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
       qm[qd] = fmaxf(fmaxf(acc[4 * qd], acc[4 * qd + 1]), fmaxf(acc[4 * qd + 2], acc[4 * qd + 3]));
-    if (fmaxf(fmaxf(qm[0], qm[1]), fmaxf(qm[2], qm[3])) < thr) return;
+    const float m = fmaxf(fmaxf(qm[0], qm[1]), fmaxf(qm[2], qm[3]));
     const bool ragged = r0 + kTR > n_rows;  // wave-uniform: the last block only
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) {
-      if (qm[qd] >= thr) {
-        if (nb + 4 > kBufCap) compact();
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = acc[4 * qd + e];
-          const uint32_t row = (uint32_t)(r0 + 8 * qd + 4 * fh + e);
-          if (v >= thr && (!ragged || row < (uint32_t)n_rows)) {
-            const uint64_t key = make_key(v, row_base + row);
-            if (key > thk) {
-              if (nb == kBufCap) compact();  // k_out + 4 > kBufCap (k = 12): one more cut mid-quad
-              lbuf[nb * kThreads] = key;
-              ++nb;
-            }
-          }
-        }
-      }
-    }
-  };
-  auto screen_loop = [&](const f32x16& acc, int r0) __attribute__((always_inline)) {
-    float m = fmaxf(acc[0], acc[1]);
-#pragma unroll
-    for (int j = 2; j < 16; ++j) m = fmaxf(m, acc[j]);
-    if (m >= thr) {
-      uint32_t pm = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) pm |= (acc[j] >= thr ? 1u : 0u) << j;
-      if (r0 + kTR > n_rows) {  // the ragged last block only
+    if (ss) {
+      if (!ragged) {
+        rm = fmaxf(rm, m);
+      } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-          if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) >= n_rows) pm &= ~(1u << j);
+          if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) rm = fmaxf(rm, acc[j]);
       }
-      while (pm) {
-        const int j = __builtin_ctz(pm);
-        pm &= pm - 1;
-        float v = acc[0];
+    }
+    if (m < thr) return;
 #pragma unroll
-        for (int jj = 1; jj < 16; ++jj) {
-          int jx = jj;
-          asm volatile("" : "+s"(jx));  // keep the select chain (an indexed read would go to scratch)
-          v = (jx == j) ? acc[jj] : v;
-        }
-        const uint32_t row = (uint32_t)(r0 + 8 * (j >> 2) + 4 * fh + (j & 3));
-        const uint64_t key = make_key(v, row_base + row);
-        if (key > thk) {
-          lbuf[nb * kThreads] = key;
-          if (++nb == kBufCap) compact();
-        }
+    for (int qd = 0; qd < 4; ++qd)
+      if (qm[qd] >= thr) screen_quad(acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3],
+                                     r0 + 8 * qd + 4 * fh, ragged);
+  };
+
+  // ---- self-seeding (see the header) ----
+  // (the seeding paths launder the lane's query index through an empty asm: otherwise LLVM hoists
+  // their 64-bit granule addresses out of the main loop, and the extra registers spill the
+  // resident fragments)
+  auto publish = [&]() __attribute__((always_inline)) {
+    const float pm = fmaxf(rm, __shfl_xor(rm, 32, 64));  // the query's max over this split's rows
+    int qq = q;
+    asm volatile("" : "+v"(qq));
+    if (!fh && qq < n_q) granule_store(pub + (int64_t)qq * n_splits + split, ((uint64_t)epoch << 32) | ord_f32(pm));
+  };
+  // the query this wave selects in the later rounds (slot j of the query block, j mod n_splits ==
+  // split, in this wave's 32; n_splits >= 32: at most one), -1 for none. Uniform.
+  auto sel_query = [&]() __attribute__((always_inline)) {
+    const int j = wave * 32 + (((split - wave * 32) % n_splits) + n_splits) % n_splits;
+    const int64_t qq = (int64_t)qb * kTQ + j;
+    return (j < wave * 32 + 32 && qq < n_q) ? qq : (int64_t)-1;
+  };
+  // The first round: every query j of this wave with j mod n_splits == split, polling (bounded)
+  // until every split's granule is there; the k-th largest published maximum becomes its seed.
+  auto select_wait = [&]() __attribute__((always_inline)) {
+    const int j0 = wave * 32 + (((split - wave * 32) % n_splits) + n_splits) % n_splits;
+#pragma unroll 1
+    for (int j = j0; j < wave * 32 + 32; j += n_splits) {
+      const int64_t qq = (int64_t)qb * kTQ + j;
+      if (qq >= n_q) break;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const uint64_t* src = pub + qq * n_splits;
+      uint32_t v0 = 0, v1 = 0;
+      const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+      for (;;) {
+        const uint64_t g0 = ln < n_splits ? granule_load(src + ln) : 0;
+        const uint64_t g1 = ln + 64 < n_splits ? granule_load(src + ln + 64) : 0;
+        const bool ok0 = (uint32_t)(g0 >> 32) == epoch, ok1 = (uint32_t)(g1 >> 32) == epoch;
+        v0 = ok0 ? (uint32_t)g0 : 0u;
+        v1 = ok1 ? (uint32_t)g1 : 0u;
+        const int n_ok = __popcll(__ballot(ok0)) + __popcll(__ballot(ok1));
+        if (n_ok >= n_splits || (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > kSeedWaitTicks) break;
+        __builtin_amdgcn_s_sleep(2);
       }
+      const uint32_t m = wave_kth(v0, v1, k_out, ln);
+      if (m != 0 && ln == 0) granule_store(seeds + qq, ((uint64_t)epoch << 32) | m);
+    }
+  };
+  auto apply_seed = [&](uint64_t g) __attribute__((always_inline)) {  // a seed granule of this launch raises thr
+    if (q < n_q && (uint32_t)(g >> 32) == epoch && (uint32_t)g != 0)
+      thr = fmaxf(thr, key_score((uint64_t)(uint32_t)g << 32));
+  };
+  auto read_wait = [&]() __attribute__((always_inline)) {  // the first round: poll (bounded) for the seeds
+    uint64_t g = 0;
+    int qq = q;
+    asm volatile("" : "+v"(qq));
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+    for (;;) {
+      g = qq < n_q ? granule_load(seeds + qq) : 0;
+      const bool ok = qq >= n_q || (uint32_t)(g >> 32) == epoch;
+      if (__ballot(!ok) == 0 || (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > kSeedWaitTicks) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    apply_seed(g);
+  };
+  // later rounds: the granules come into the wave's scratch by LDS-DMA one stage before their use
+  auto sel_fetch = [&](int64_t qq) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    granules_to_lds(pub + qq * n_splits, (uint32_t)n_splits * 8, wscr + 1024, ln);
+  };
+  auto sel_use = [&](int64_t qq) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint64_t* g = reinterpret_cast<const uint64_t*>(wscr + 1024);
+    const uint64_t g0 = g[ln], g1 = g[ln + 64];  // past n_splits: zeros
+    const uint32_t v0 = (uint32_t)(g0 >> 32) == epoch ? (uint32_t)g0 : 0u;
+    const uint32_t v1 = (uint32_t)(g1 >> 32) == epoch ? (uint32_t)g1 : 0u;
+    const uint32_t m = wave_kth(v0, v1, k_out, lane);
+    if (m != 0 && lane == 0) granule_store(seeds + qq, ((uint64_t)epoch << 32) | m);
+  };
+  auto read_fetch = [&]() __attribute__((always_inline)) {  // the wave's 32 seeds (256 B)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    granules_to_lds(seeds + qw0, 256, wscr + 2048, ln);
+  };
+  auto read_use = [&]() __attribute__((always_inline)) {
+    int f = fr;
+    asm volatile("" : "+v"(f));
+    apply_seed(reinterpret_cast<const uint64_t*>(wscr + 2048)[f]);
+  };
+  // block 0's raw scores parked in the upper half of the lane buffer (entries 8 .. 15, two floats
+  // each) until the first seed; replayed quad by quad from the bottom while the appends fill the
+  // buffer from entry 0: after quad qd at most 4 (qd + 1) keys, below entry 8 + 2 (qd + 1) — the
+  // appends never reach a quad not yet read.
+  auto park = [&](const f32x16& acc) __attribute__((always_inline)) {
+    uint64_t* const lbuf = lb();
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      lbuf[(8 + e) * kThreads] = ((uint64_t)__float_as_uint(acc[2 * e + 1]) << 32) | __float_as_uint(acc[2 * e]);
+  };
+  auto replay = [&](int r0) __attribute__((always_inline)) {
+    asm volatile("" : "+s"(r0));  // (not loop-invariant to LLVM: it would hoist all 16 row keys and spill them)
+    const bool ragged = r0 + kTR > n_rows;
+    uint64_t* const lbuf = lb();
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      const uint64_t a = lbuf[(8 + 2 * qd) * kThreads], b = lbuf[(9 + 2 * qd) * kThreads];
+      const float v0 = __uint_as_float((uint32_t)a), v1 = __uint_as_float((uint32_t)(a >> 32));
+      const float v2 = __uint_as_float((uint32_t)b), v3 = __uint_as_float((uint32_t)(b >> 32));
+      if (fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)) >= thr) screen_quad(v0, v1, v2, v3, r0 + 8 * qd + 4 * fh, ragged);
     }
   };
 
-  // Waves 4-7 (the second wave of every SIMD) run one stage behind waves 0-3, so the two waves of a
-  // SIMD never reach a block end together: a wave screens a finished block at the start of the
-  // next interval, before its next MFMA, while its partner's MFMAs keep the SIMD's matrix pipe busy
-  // (in lock-step both would stop the pipe for the screening at every block end).
-  // Interval j (after sync j): waves 0-3 multiply stage j, waves 4-7 stage j - 1.
   // Sync j: this wave's pieces of stage j landed (stage j + 1 may stay in flight), then the
-  // barrier: everyone's stage j landed, and everyone is done with stage j - 2 (waves 4-7 finished
-  // it in interval j - 1), whose slot takes stage j + 2. A stage is issued two intervals ahead.
-  // SYNC = 2: one barrier per 32-row block instead of one per stage. At a block's first stage e
-  // a wave waits for ALL its pieces in flight (stages e and e + 1: vmcnt(0)), then the barrier:
-  // everyone's e and e + 1 landed and everyone finished stage e - 1, so e + 2 may take stage
-  // e - 2's slot now and e + 3 stage e - 1's at the block's second stage, which needs neither a
-  // wait nor a barrier. The block's screening (after the barrier) then has two stages of MFMAs,
-  // not one, to even out between the waves before the next barrier; the price is waiting for
-  // stage e + 1 one stage after its issue instead of two.
-  auto stage_sync_blk = [&](int j) __attribute__((always_inline)) {
-    if (!(j & 1)) {
-      wait_vm<0>();
-      lds_barrier();
-    }
-    if (j + 2 < n_st) issue(j + 2);
-  };
+  // barrier: everyone's stage j landed, and everyone is done with stage j - 1, whose slot takes
+  // stage j + 2 (a 3-slot ring, a stage issued two intervals ahead).
   auto stage_sync = [&](int j) __attribute__((always_inline)) {
-    if constexpr (SYNC == 2) {
-      stage_sync_blk(j);
-      return;
-    }
     if (!(ABL & ABL_NOWAIT)) {
       if (j + 1 < n_st)
         wait_vm<C::kPPW>();
@@ -268,22 +427,25 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
         wait_vm<0>();
     }
     if (!(ABL & ABL_NOBARRIER)) lds_barrier();
-    if (j + 2 < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + 2);
   };
-  // A fragment of k16 step s of stage st: k-tile s / 4, chunk 2 (s % 4) + fh of row fr
-  const int a_row = fr * kRowBytes;
-  const int a_x = (fr >> 1) & 7;
+  // A fragment of k16 step s of stage st: k-tile s / 4, logical chunk 2 (s % 4) + fh of row fr,
+  // stored at physical chunk (2 (s % 4) + fh) ^ ((fr >> 1) & 7) = 2 ((s % 4) ^ h) + (fh ^ a0),
+  // h = (fr >> 2) & 3, a0 = (fr >> 1) & 1. The byte offset is one v_xad_u32 per read from two
+  // per-lane values (the four precomputed offsets would cost two more live registers).
+  const int a_base = fr * kRowBytes + ((fh ^ ((fr >> 1) & 1)) << 4);
+  const int a_h = ((fr >> 2) & 3) << 5;
   auto frag = [&](int st, int s) __attribute__((always_inline)) {
     if constexpr ((ABL & ABL_NOREAD) != 0) return qf[(s + 5) % C::kNS];  // MFMA + issue only
-    const unsigned char* slot = smem + (st & (kSlots - 1)) * C::kStage;
-    return *reinterpret_cast<const u32x4*>(slot + (s >> 2) * kKt + a_row + (((2 * (s & 3) + fh) ^ a_x) << 4));
+    const unsigned char* slot = slot_of(st);
+    int hx;  // a_h ^ 32 (s % 4), per read (volatile: never hoisted or shared between reads)
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(hx) : "i"((s & 3) << 5), "v"(a_h));
+    return *reinterpret_cast<const u32x4*>(slot + (s >> 2) * kKt + (hx + a_base));
   };
   static_assert(C::kSS % 3 == 0, "three fragment registers rotate evenly over a stage");
-  const int lag = (SYNC == 1 && wave >= 4) ? 1 : 0;
   constexpr bool skip_screen = (ABL & ABL_NOSCREEN) != 0;
   f32x16 acc;
   u32x4 fa[3];
-  // the stage's 24 steps: step t prefetches step t + 2 and multiplies step t; H = block half
+  // the stage's 24 steps: step t prefetches step t + 2 and multiplies step t; H = stage of the block
   auto stage_mma = [&](auto H, int st) __attribute__((always_inline)) {
     constexpr int h = decltype(H)::value;
 #pragma unroll
@@ -300,40 +462,95 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto finish_block = [&](int st_done) __attribute__((always_inline)) {  // st_done: the block's 2nd stage
+  auto finish_block = [&](int bi, int64_t sq) __attribute__((always_inline)) {  // bi: the block just multiplied
     if constexpr (skip_screen) {  // GEMM only: the chain kept live (rule 17), no top-k
       asm volatile("" ::"v"(acc));
       return;
     }
-    if constexpr (SCR == 1)
-      screen_quads(acc, (b_begin + (st_done >> 1)) * kTR);
-    else
-      screen_loop(acc, (b_begin + (st_done >> 1)) * kTR);
+    const int r0 = (b_begin + bi) * kTR;
+    if (ss && bi == 0) {  // the first round's sample: park the scores, publish the maxima
+      park(acc);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)  // block 0 is never ragged (>= 2 blocks per split) but check anyway
+        if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) rm = fmaxf(rm, acc[j]);
+      publish();
+      return;
+    }
+    screen_quads(acc, r0);
+    if (ss_rounds) {
+      if (ss_round(bi)) publish();
+      if (sq >= 0) sel_use(sq);
+      if (bi >= 2 * kD && ss_round(bi - 2 * kD)) read_use();
+    }
+  };
+  // The first seed (bounded waits) at the end of block 1, before the block's screening: its 16
+  // accumulators wait in LDS (12 in the ring slot that is free then — stage j - 1's, whose refill
+  // is issued only after this path — and 4 in the wave's scratch), so the waits and the replay of
+  // block 0 hold no accumulator registers; the main loop has none to spare.
+  auto first_seed = [&](int j) __attribute__((always_inline)) {
+    float* const pa = reinterpret_cast<float*>(slot_of(j - 1)) + tid * 4;
+    float* const pb = reinterpret_cast<float*>(wscr) + lane * 4;
+    auto at = [&](int i) __attribute__((always_inline)) { return i < 12 ? pa + (i >> 2) * kThreads * 4 : pb; };
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) *reinterpret_cast<f32x4*>(at(i)) = f32x4{acc[i], acc[i + 1], acc[i + 2], acc[i + 3]};
+    asm volatile("" ::: "memory");
+    select_wait();
+    read_wait();
+    replay(b_begin * kTR);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(at(i));
+      acc[i] = v[0];
+      acc[i + 1] = v[1];
+      acc[i + 2] = v[2];
+      acc[i + 3] = v[3];
+    }
   };
 #pragma unroll 1
   for (int j = 0; j <= n_st; ++j) {
     stage_sync(j);
-    const int st = j - lag;
-    if (!live) continue;
-    const bool mma = st >= 0 && st < n_st;
-    if (mma) {  // the stage's first fragments: in flight under the screening below
-      fa[0] = frag(st, 0);
-      fa[1] = frag(st, 1);
+    const bool seed_now = ss && j == 2 * C::kSPB;  // uniform
+    const bool bend = j >= C::kSPB && j % C::kSPB == 0;  // block j / kSPB - 1 ended with stage j - 1
+    // this round's granules go to LDS at the last stage sync of the block that uses them (before
+    // the stage's DMA: the next sync's counted wait covers them)
+    int64_t sq = -1;
+    if (ss_rounds && live && (j + 1) % C::kSPB == 0 && j + 1 >= C::kSPB) {
+      const int bu = (j + 1) / C::kSPB - 1;  // the block whose end uses them
+      if (bu >= kD && ss_round(bu - kD)) {
+        sq = sel_query();
+        if (sq >= 0) sel_fetch(sq);
+      }
+      if (bu >= 2 * kD && ss_round(bu - 2 * kD)) read_fetch();
     }
-    if (st >= 2 && !(st & 1)) finish_block(st - 1);  // the block that ended with stage st - 1
+    if (seed_now) {
+      if (live) first_seed(j);
+      lds_barrier();  // every wave's parked accumulators are back before the slot is refilled
+    }
+    if (j + 2 < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + 2);
+    if (!live) continue;
+    const bool mma = j < n_st;
+    if (mma) {  // the stage's first fragments: in flight under the screening below
+      fa[0] = frag(j, 0);
+      fa[1] = frag(j, 1);
+    }
+    if (bend) {
+      const int bi = j / C::kSPB - 1;
+      finish_block(bi, (ss_rounds && bi >= kD && ss_round(bi - kD)) ? sel_query() : (int64_t)-1);
+    }
     if (mma) {
-      if (st & 1)
-        stage_mma(std::integral_constant<int, 1>{}, st);
+      if (C::kSPB == 1 || !(j & 1))
+        stage_mma(std::integral_constant<int, 0>{}, j);
       else
-        stage_mma(std::integral_constant<int, 0>{}, st);
+        stage_mma(std::integral_constant<int, 1>{}, j);
     }
   }
-  if (live && lag && n_st > 0) finish_block(n_st - 1);  // waves 4-7: their last block
 
   // this lane's buffered keys, sorted (the query registers are dead from here on)
   uint64_t L[KCAP];
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  uint64_t* const lbuf = lb();
 #pragma unroll 1
   for (int c = 0; c < nb; ++c) list_insert<KCAP>(L, lbuf[c * kThreads]);
   // lane fr + 32 hands its list to lane fr through the (idle) ring
@@ -359,77 +576,71 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 }
 
 bool supported(int dtype, int d_pad_bytes, int k) {
-  return (dtype == AHR_BF16 || dtype == AHR_F16) && d_pad_bytes == 12 * kRowBytes && k >= 1 && k <= 12 &&
-         k < kBufCap;
+  return (dtype == AHR_BF16 || dtype == AHR_F16) && (d_pad_bytes == 12 * kRowBytes || d_pad_bytes == 6 * kRowBytes) &&
+         k >= 1 && k <= 12 && k < kBufCap;
 }
 
-
-int frag_mode(int k, int flags) { return use16(k, flags) ? 16 : 32; }
-
-void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes, int k, uint8_t* qfrag, int flags,
+void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes, uint8_t* qfrag, uint32_t* epoch,
                  hipStream_t s) {
-  if (!use16(k, flags)) {  // the 32x32x16 kernel's layout: 32-query groups, k16 steps
-    const int ns = d_pad_bytes / 32;
-    const int64_t n16 = (int64_t)((B + 31) / 32) * ns * 64;
-    hipLaunchKernelGGL(frag_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, s, qbuf, row_stride, n16, ns,
-                       qfrag);
-    return;
-  }
-  launch_frag16(qbuf, row_stride, B, d_pad_bytes, qfrag, s);
+  const int ns = d_pad_bytes / 32;
+  const int64_t n16 = (int64_t)((B + 31) / 32) * ns * 64;
+  hipLaunchKernelGGL(frag_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, s, qbuf, row_stride, n16, ns,
+                     qfrag, epoch);
 }
 
-template <int DT, int KCAP, int SYNC, int SCR, int ABL = 0>
+template <int DT, int NKT, int KCAP, int ABL = 0, bool ROUNDS = false>
 void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
-              int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, hipStream_t s) {
+              int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, uint64_t* pub,
+              uint64_t* seeds, const uint32_t* epoch, hipStream_t s) {
   if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
     const int abl = ((flags & kFlagSkipEpilogue) ? ABL_NOSCREEN : 0) | ((flags & kFlagNoLoads) ? ABL_NOLOADS : 0) |
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
                     ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0);
 #define AHR_QRES_ABL(V) \
-  case V: launch_t<DT, KCAP, SYNC, SCR, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s); return;
+  case V: launch_t<DT, NKT, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, seeds, epoch, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       default: break;
     }
 #undef AHR_QRES_ABL
   }
-  constexpr auto kern = &topk_qres_kernel<DT, 12, KCAP, SYNC, SCR, ABL>;
+  constexpr auto kern = &topk_qres_kernel<DT, NKT, KCAP, ABL, ROUNDS>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), Cfg<12>::kLds);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), Cfg<12>::kLds, s, rows, qfrag,
-                     row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags);
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), Cfg<NKT>::kLds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), Cfg<NKT>::kLds, s, rows, qfrag,
+                     row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, seeds, epoch);
 }
 
-template <int DT, int KCAP>
-void launch_s(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
-              int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, hipStream_t s) {
-  if (flags & kFlagQresStagger)
-    launch_t<DT, KCAP, 1, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
-  else if (flags & kFlagQresBlkSync)
-    launch_t<DT, KCAP, 2, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
-  else if (flags & kFlagQresScreenLoop)
-    launch_t<DT, KCAP, 0, 0>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+template <int DT, int NKT>
+void launch_k(int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
+              uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
+              uint64_t* pub, uint64_t* seeds, const uint32_t* epoch, hipStream_t s) {
+  if (k <= 8)
+    launch_t<DT, NKT, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub,
+                         seeds, epoch, s);
   else
-    launch_t<DT, KCAP, 0, 1>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+    launch_t<DT, NKT, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags,
+                          pub, seeds, epoch, s);
 }
 
-void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
-            uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
-            hipStream_t s) {
-  if (use16(k, flags)) {
-    launch16(dtype, k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags, s);
-    return;
-  }
+void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int d_pad_bytes,
+            int n_rows, int B, uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks,
+            int flags, uint64_t* pub, uint64_t* seeds, const uint32_t* epoch, hipStream_t s) {
+  const bool wide = d_pad_bytes == 12 * kRowBytes;
   if (dtype == AHR_BF16) {
-    if (k <= 8)
-      launch_s<DT_BF16, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+    if (wide)
+      launch_k<DT_BF16, 12>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
+                            pub, seeds, epoch, s);
     else
-      launch_s<DT_BF16, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+      launch_k<DT_BF16, 6>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
+                           pub, seeds, epoch, s);
   } else {
-    if (k <= 8)
-      launch_s<DT_F16, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+    if (wide)
+      launch_k<DT_F16, 12>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
+                           pub, seeds, epoch, s);
     else
-      launch_s<DT_F16, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, s);
+      launch_k<DT_F16, 6>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
+                          pub, seeds, epoch, s);
   }
 }
 

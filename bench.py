@@ -59,8 +59,12 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["hotpot90k", "synth5m"], default=None,
-                    help="default: hotpot90k at N=1, synth5m (row-sharded) at N>1")
+    ap.add_argument("--workload", choices=["hotpot90k", "synth5m", "env"], default=None,
+                    help="default: hotpot90k at N=1, synth5m (row-sharded) at N>1; env = configs[4], the RL "
+                         "environment loop (VecAHRAGGymEnv, replicas: --envs per GPU)")
+    ap.add_argument("--envs", type=int, default=1024, help="--workload env: environments per GPU")
+    ap.add_argument("--no-sublines", action="store_true",
+                    help="N=1 hotpot90k: skip the synth5m (configs[2]) and C5 env (configs[4]) sub-lines")
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--dtype", choices=["bf16", "f16", "f32"], default=None)
@@ -248,8 +252,9 @@ def time_queries(ix, q, k: int, steps: int, warmup: int, inflight: int, dev):
 
 
 def read_traffic(kernel: str, workload: str, batch: int):
-    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary (profiles/) measured
-    on this workload and batch (else None)."""
+    """(per-launch HBM bytes of `kernel`, the summary file) from the newest committed PMC summary
+    (profiles/) measured on this workload and batch, else (None, None). A committed measurement,
+    not this run's: the file is reported beside the value."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*", "pmc_traffic.json")), reverse=True)
     paths.append(os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     for path in paths:
@@ -262,8 +267,8 @@ def read_traffic(kernel: str, workload: str, batch: int):
             continue
         v = data.get(kernel, {}).get("hbm_bytes_per_launch")
         if v is not None:
-            return v
-    return None
+            return v, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def roofline(plan: dict, dtype: str, B: int, n_rows: int, d: int, k: int, tile_ms: float, workload: str) -> dict:
@@ -282,6 +287,7 @@ def roofline(plan: dict, dtype: str, B: int, n_rows: int, d: int, k: int, tile_m
     # small batches are bound by the corpus stream
     hbm_bound = flops / alg_bytes < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
     hbm_gbs = alg_bytes / (tile_ms * 1e-3) / 1e9
+    traffic, traffic_src = read_traffic(kname, workload, B)
     return {
         "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} "
                   f"Q.N^T + top-k, {plan['kernel']})",
@@ -290,7 +296,8 @@ def roofline(plan: dict, dtype: str, B: int, n_rows: int, d: int, k: int, tile_m
         "peak": HBM_PEAK_GBS if hbm_bound else peak,
         "unit": "GB/s" if hbm_bound else "TFLOP/s",
         "frac": round(hbm_gbs / HBM_PEAK_GBS if hbm_bound else achieved_tf / peak, 4),
-        "traffic": read_traffic(kname, workload, B),
+        "traffic": traffic,
+        "traffic_source": traffic_src,
         "algorithmic_flops_per_launch": flops,
         "algorithmic_bytes_per_launch": alg_bytes,
         "hbm_equiv_GBs": round(hbm_gbs, 1),
@@ -299,7 +306,80 @@ def roofline(plan: dict, dtype: str, B: int, n_rows: int, d: int, k: int, tile_m
     }
 
 
+def synth5m_line(args, dev) -> dict:
+    """configs[2] beside the N = 1 headline: the 5M x 768 fp16 corpus, B = 1024, top-k, on this GPU
+    (same timing as the headline: inflight batches, then a serial pass with stage events)."""
+    spec, dtype, B, k = SYNTH_5M, "f16", args.batch, args.k
+    corpus = SyntheticCorpus(spec, dev)
+    N, d = spec.n_rows, spec.dim
+    ix = DenseIndex(d, N, dtype=dtype, device=dev)
+    for s0, x in corpus.entity_chunks():
+        ix.upsert(x, start=s0)
+    q, _ = corpus.queries(B, None, salt=0)
+    steps = max(3, min(args.steps, 20))
+    dt, prof, res = time_queries(ix, q, k, steps, max(1, min(args.warmup, 3)), max(1, args.inflight), dev)
+    calls = max(1, prof["calls"])
+    tile_ms = prof["ms_sum"]["tile_topk"] / calls
+    nq = min(128, B)
+    _, exact = numpy_topk_chunked(corpus.entity_chunks(), q[:nq].cpu().numpy(), k)
+    plan = ix.plan(B, k)
+    ix.close()
+    return {
+        "workload": "synth5m: BASELINE configs[2], 5M x 768 fp16, synthetic (SURVEY §8d generator)",
+        "value": round(B * steps / dt, 1), "unit": "queries/s", "steps": steps,
+        "ms_per_step": round(dt / steps * 1e3, 4), "recall_at_10": round(recall_at_k(
+            res[1][:nq].cpu().numpy().astype(np.int64), exact), 4),
+        "launch": plan,
+        "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
+        "roofline": roofline(plan, dtype, B, N, d, k, tile_ms, "synth5m"),
+    }
+
+
+def env_line(args, dev, rank: int = 0, world: int = 1) -> dict:
+    """configs[4]: the RL environment loop (tools/bench_env.py measure): VecAHRAGGymEnv over the
+    130k-node HotpotQA-shaped graph, `--envs` environments per GPU, plus the drop-in single-env rate."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_env  # noqa: E402
+    return bench_env.measure(dev, args.envs, 6, single=32, rank=rank, world=world, total_envs=args.envs * world,
+                             backend=args.backend)
+
+
+def run_env(args) -> None:
+    """--workload env: configs[4] as the bench line (replicas: every GPU its own graph copy and
+    --envs environments, no collective on the data path; weak scaling)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    r = env_line(args, dev, rank, world)
+    if rank == 0:
+        steps = r["steps_per_episode"] + 1  # the reset counts as one env step, as in the rate
+        out = {
+            "metric": r["metric"], "value": r["vec_env_steps_per_s"], "unit": "env-steps/s", "n_gpus": world,
+            "steps": steps, "warmup": steps, "ms_per_step": round(r["episode_s"] / steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": r["data"],
+            "config": {"workload": "env: BASELINE configs[4], 2-hop expand + re-score inside the RL env loop",
+                       "envs_per_gpu": r["envs_per_gpu"], "parallelism": r["parallelism"], "graph": r["graph"]},
+            "c5": r, "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def run(args) -> None:
+    if args.workload == "env":
+        run_env(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -483,7 +563,11 @@ def run(args) -> None:
                 "serial_ms_per_step": round(dt_serial / args.steps * 1e3, 4) if dt_serial else None,
                 "recall_queries": nq,
                 "threshold_seed": (f"cluster probe ({clusters['clusters']} clusters, built in {clusters['build_s']} s)"
-                                   if clusters else "sampled pre-pass"),
+                                   if clusters else
+                                   ("self-seeded inside the register-resident kernel (published split maxima; "
+                                    "no pre-pass launch)" if plan["kernel"] == "qres256"
+                                    and not args.debug_flags & (1 << 26) and args.sample_rows != 0
+                                    else "sampled pre-pass")),
             },
             "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
             "roofline": roofline(plan, dtype, B, n_local, d, k, tile_ms, workload),
@@ -526,6 +610,12 @@ def run(args) -> None:
                     "stages_ms_per_step": {kk: round(v / b_calls, 4) for kk, v in b_prof["ms_sum"].items()},
                     "roofline": roofline(b_plan, dtype, b, N, d, k, b_prof["ms_sum"]["tile_topk"] / b_calls,
                                          workload)})
+        if world == 1 and workload == "hotpot90k" and not args.no_sublines:
+            # configs[2] and configs[4] under the driver's clock, beside the configs[1] headline
+            local.close()
+            index = None
+            out["synth5m"] = synth5m_line(args, dev)
+            out["c5_env"] = env_line(args, dev)
         if world == 1 and not args.no_cpu_baseline:
             nc = min(len(q), 1024)
             if rows is not None:
@@ -537,7 +627,8 @@ def run(args) -> None:
             out["cpu_baseline"] = cpu_baseline(host_rows, q[:nc].cpu().numpy(), k, args.cpu_seconds, workload)
             del host_rows
         print(json.dumps(out), flush=True)
-    index.close()
+    if index is not None:
+        index.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -124,35 +124,31 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
                          int P, const int64_t* list_off, const int32_t* list_rows, int min_rows, float* thr,
                          void* stream);
 
-/* Kernel-selection switches (A/B measurements; results stay correct): 8 = always the
- * 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile kernel at any
- * batch (k <= 16), 64 = the 256x128 lane kernel (k <= 16), 2048 = no query-resident kernel,
- * 4096 = the query-resident kernel wherever it applies, 32768 = the 256x256 16x16x32 kernel,
- * 65536 = the small-batch streaming kernel up to B = 64, 131072 = the k-blocked 256x256 kernel
- * wherever it applies, 262144 = never the k-blocked kernels, 524288 = the k-blocked 256x128 kernel
- * (two workgroups per CU) wherever it applies, 4194304 = small batches merge through a merge
- * launch instead of the last-workgroup fold, 16384 = tilelane without the cross-tile prefetch,
- * 1 << 23 = the 256-query register-resident kernel (qres256) wherever it applies (bf16/f16,
- * d_pad 768, k <= 12), 1 << 26 = qres256 with waves 4-7 one stage behind, 1 << 27 = qres256's
- * select-chain screening, 1 << 28 / 1 << 29 = qres256's 16x16x32 forms (8 waves x 32 queries /
- * 4 waves x 64 queries; k <= 10), 1 << 30 = kb256 without split pacing, 1 << 31 = qres256
- * (32x32x16 form) with one barrier per 32-row block instead of one per stage. 2048 keeps the
- * query-resident kernels (qkv and qres256) out of the plan.
+/* Kernel-selection switches (A/B measurements; results stay correct), a 32-bit unsigned flag word:
+ * 8 = always the 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile
+ * kernel at any batch (k <= 16), 2048 = no query-resident kernel (qkv or qres256), 4096 = the
+ * query-resident kernel (qkv) wherever it applies, 16384 = tilelane without the cross-tile
+ * prefetch, 32768 = the 256x256 16x16x32 kernel, 131072 = the k-blocked 256x256 kernel wherever it
+ * applies, 262144 = never the k-blocked kernel, 1 << 22 = small batches merge through a merge
+ * launch instead of the last-workgroup fold, 1 << 23 = the 256-query register-resident kernel
+ * (qres256) wherever it applies (bf16/f16, d_pad 384 or 768, k <= 12), 1 << 26 = qres256 seeded
+ * by the sampled pre-pass launch instead of seeding itself, 1 << 27 = qres256's self-seeding with
+ * its first round only.
  * Cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
  * only, 512 = operands of the first tile only, 1024 = loads never waited for, 1048576 / 2097152 =
  * k-blocked tiles read from tile 0 / the split's first tile, 1 << 24 / 1 << 25 = qres256 without
  * stage barriers / LDS fragment reads) are accepted only by the ablation
- * build (-DAHR_ABLATION, __graft_entry__.build_ablation); the shipped library returns AHR_EUNSUP. */
-int ahr_index_set_debug_flags(ahr_index* ix, int flags);
+ * build (-DAHR_ABLATION, __graft_entry__.build_ablation); the shipped library returns AHR_EUNSUP.
+ * Unknown bits return AHR_EINVAL. */
+int ahr_index_set_debug_flags(ahr_index* ix, uint32_t flags);
 
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
  * *kernel: 0 = 128x128 tile kernel (cooperative screening; k > 16), 1 = 256x256 lane kernel
- * (k <= 16, B >= 6144), 2 = 256x128 lane kernel, 3 = 128x128 lane-local tile kernel (k <= 16,
- * B < 6144), 5 = query-resident kernel (bf16/f16, 2048 <= B <= 8192), 6 = 256x256 16x16x32
- * kernel (opt-in), 7 = small-batch streaming kernel (bf16/f16, B <= 16, k <= 16), 8 = k-blocked
- * 256x256 kernel (bf16/f16, k <= 16, from 512k corpus rows), 9 = k-blocked 256x128 kernel (opt-in),
- * 10 = 256-query register-resident kernel (bf16/f16, d_pad 768, k <= 12, B >= 512, below 512k
- * rows, with the threshold pre-pass). */
+ * (k <= 16, B >= 6144), 3 = 128x128 lane-local tile kernel (k <= 16, B < 6144), 5 = query-resident
+ * kernel (opt-in), 6 = 256x256 16x16x32 kernel (opt-in), 7 = small-batch streaming kernel
+ * (bf16/f16, B <= 16, k <= 16), 8 = k-blocked 256x256 kernel (bf16/f16, k <= 16, from 512k corpus
+ * rows), 10 = 256-query register-resident kernel (bf16/f16, d_pad 384 or 768, k <= 12, B >= 512,
+ * 32k to 512k rows, self-seeded). Ids 2, 4 and 9 are retired. */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 

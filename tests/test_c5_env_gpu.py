@@ -14,7 +14,6 @@ Reference loop: /root/reference/src/ah_rag/agent/policy_ppo.py:145,163-214 over
 /root/reference/src/ah_rag/agent/environment.py:393-480.
 """
 import json
-import os
 
 import numpy as np
 import pytest
@@ -39,16 +38,17 @@ def _norm(x):
 def hotpot_env(cuda, tmp_path_factory):
     import torch
     from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph, install_vectors
-    os.environ["AHR_INDEX_DTYPE"] = "f32"  # the drop-in default (exact mode)
-    corpus = SyntheticCorpus(HOTPOT_90K, cuda)
-    rows = corpus.rows()
-    vectors = rows.cpu().numpy()
-    hg, ids = build_hotpot_graph(corpus, np.random.default_rng(20251003))
-    db = str(tmp_path_factory.mktemp("c5") / "vector_db")
-    install_vectors(hg, ids, vectors, db)
-    q, _ = corpus.queries(N_ENVS, rows, salt=3)
-    torch.cuda.synchronize()
-    return hg, ids, vectors, q.cpu().numpy()
+    with pytest.MonkeyPatch.context() as mp:  # module-scoped: restored after this module
+        mp.setenv("AHR_INDEX_DTYPE", "f32")  # the drop-in default (exact mode)
+        corpus = SyntheticCorpus(HOTPOT_90K, cuda)
+        rows = corpus.rows()
+        vectors = rows.cpu().numpy()
+        hg, ids = build_hotpot_graph(corpus, np.random.default_rng(20251003))
+        db = str(tmp_path_factory.mktemp("c5") / "vector_db")
+        install_vectors(hg, ids, vectors, db)
+        q, _ = corpus.queries(N_ENVS, rows, salt=3)
+        torch.cuda.synchronize()
+        yield hg, ids, vectors, q.cpu().numpy()
 
 
 def test_c5_hotpot_graph_shape(hotpot_env):

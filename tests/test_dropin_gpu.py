@@ -29,19 +29,19 @@ def _norm(x):
 
 @pytest.fixture(scope="module")
 def workdir(tmp_path_factory, cuda):
-    os.environ["AHR_ENCODER"] = "hash"
-    os.environ["AHR_INDEX_DTYPE"] = "f32"
     from ah_rag.graph.hierarchical_graph import HierarchicalGraph
     d = tmp_path_factory.mktemp("dropin")
     shutil.copytree(os.path.join(GOLDEN, "reference_graph"), d / "graph")
-    cwd = os.getcwd()
-    os.chdir(d)
-    hg = HierarchicalGraph.load("graph")
-    # the fixture graph's meta already lists every entity/summary key (it was saved after the
-    # reference built its index), so rebuild the collection without the upsert-only skip
-    hg.build_vector_index(db_path="vector_db", layers={0, 1}, upsert_only=False, reset=True)
-    yield d, hg
-    os.chdir(cwd)
+    # the settings hold for this module only (restored after it: no leak into later modules)
+    with pytest.MonkeyPatch.context() as mp:
+        mp.setenv("AHR_ENCODER", "hash")
+        mp.setenv("AHR_INDEX_DTYPE", "f32")
+        mp.chdir(d)
+        hg = HierarchicalGraph.load("graph")
+        # the fixture graph's meta already lists every entity/summary key (it was saved after the
+        # reference built its index), so rebuild the collection without the upsert-only skip
+        hg.build_vector_index(db_path="vector_db", layers={0, 1}, upsert_only=False, reset=True)
+        yield d, hg
 
 
 def test_hash_encoder_matches_fixture_encoder():
@@ -66,6 +66,17 @@ def test_search_matches_reference(workdir):
         assert isclose_dicts(_norm(got), c["result"]), (c["query"], c["params"])
         n += 1
     assert n > 80
+
+
+def test_search_topk_beyond_count(workdir):
+    """top_k above the index count (and above AHR_MAX_K_LARGE): Chroma returns every row, so does
+    the drop-in (tests/golden/make_golden_bigk.py, the reference's own search over 313 rows)."""
+    d, hg = workdir
+    cases = _load("search_bigk_cases.json")["cases"]
+    assert any(c["params"]["top_k"] > 4096 for c in cases)
+    for c in cases:
+        got = hg.search(c["query"], return_cluster=c["return_cluster"], **c["params"])
+        assert isclose_dicts(_norm(got), c["result"]), (c["query"], c["params"])
 
 
 def test_search_batch_equals_single(workdir):

@@ -1,13 +1,16 @@
 """The 256-query register-resident kernel (csrc/ahr_qres.hip) — the default B >= 512 bf16/f16 plan at
-d = 768, k <= 12 (the C2 headline shape; reference src/ah_rag/graph/hierarchical_graph.py:714).
+d = 768 and 384, k <= 12 (the C2 headline shape; reference src/ah_rag/graph/hierarchical_graph.py:714).
 
-Two forms, each chaining the MFMA steps of an existing kernel in the same k order, so scores AND
-rows must be bitwise equal to that kernel: the default 32x32x16 form to the lane-local tile kernel
-(topk_tilelane_kernel), the v_mfma_f32_16x16x32 form (flag 1 << 28, k <= 10) to the 256x256 tile
-kernel (topk_t256_kernel, itself bitwise equal to the k-blocked and small-batch kernels) — including
-ragged row and query blocks, splits with no rows, no threshold seed (every score a candidate: the
-survivor buffers' compaction path), adversarial row order, exact ties (lowest row id first) and
-row-base offsets. Against the f64 oracle the half-precision tolerance of test_dense_gpu.py applies.
+It chains the MFMA steps of the lane-local tile kernel (topk_tilelane_kernel) in the same k order,
+so scores AND rows must be bitwise equal to it — with its admission threshold seeded by itself
+(the default: splits publish per-query maxima, the k-th largest becomes the seed), by the sampled
+pre-pass launch (flag 1 << 26), or not at all (sample rows 0: every score a candidate, the survivor
+buffers' compaction path) — including ragged row and query blocks, splits with no rows, adversarial
+row order (the records all in the last split, or every row a new record), exact ties (lowest row
+id first), consecutive launches with changing batch shapes (stale granules of another launch) and
+row-base offsets. A seed above a query's true k-th score would drop rows: the bitwise comparisons
+are the validity check. Against the f64 oracle the half-precision tolerance of test_dense_gpu.py
+applies.
 """
 import numpy as np
 import pytest
@@ -18,9 +21,7 @@ from oracle import dense_ref as dr
 pytestmark = pytest.mark.gpu
 
 QRES = 1 << 23      # plan the register-resident kernel wherever it applies
-QRES16 = 1 << 28    # ... in its 16x16x32 form
-QRES4W = 1 << 29    # ... in its 16x16x32 form with 4 waves of 64 queries
-QRES_BLK = 1 << 31  # ... (32x32x16 form) with one barrier per block instead of per stage
+PREPASS = 1 << 26   # ... seeded by the sampled pre-pass launch instead of by itself
 TILELANE = 32       # the lane-local 128x128 tile kernel at any batch
 T256 = 32768        # the 256x256 16x16x32 tile kernel
 
@@ -41,39 +42,38 @@ def _run(ix, Q, k, flags, kernel):
 
 
 def _check_forms(ix, Q, k):
-    """Both forms against their reference kernels, bitwise; returns the default (32x32x16) form's
-    result. The 16x16x32 form covers k <= 10 (k = 11, 12 fall back to the 32x32x16 form)."""
+    """Self-seeded and pre-pass-seeded launches against the tile kernel, bitwise; returns the
+    self-seeded (default) result."""
     a = _run(ix, Q, k, QRES, "qres256")
     d = _run(ix, Q, k, TILELANE, "tilelane128")
     np.testing.assert_array_equal(a[1], d[1])
     np.testing.assert_array_equal(a[0], d[0])
-    e = _run(ix, Q, k, QRES | QRES_BLK, "qres256")
+    e = _run(ix, Q, k, QRES | PREPASS, "qres256")
     np.testing.assert_array_equal(e[1], a[1])
     np.testing.assert_array_equal(e[0], a[0])
-    ref = _run(ix, Q, k, T256, "t256") if k <= 10 else a
-    for form in (QRES16, QRES4W):
-        c = _run(ix, Q, k, QRES | form, "qres256")
-        np.testing.assert_array_equal(c[1], ref[1])
-        np.testing.assert_array_equal(c[0], ref[0])
     return a
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("n,B,k,sample", [
-    (90000, 1024, 10, 8192),  # the C2 shape
-    (40001, 512, 10, 8192),   # ragged last row block
-    (40001, 700, 1, 8192),    # ragged query block (a partly live wave, whole dead waves), k = 1
-    (40001, 1024, 12, 0),     # no seed: compaction from the first block on
-    (33000, 2048, 8, 8192),
-    (5000, 600, 10, 0),
-    (300, 512, 5, 0),         # 10 row blocks over 8 splits, queries 300.. of the second block dead
+@pytest.mark.parametrize("n,B,k,sample,d", [
+    (90000, 1024, 10, 8192, 768),  # the C2 shape
+    (90000, 1024, 10, 8192, 384),  # ... at the reference's default width
+    (40001, 512, 10, 8192, 768),   # ragged last row block; 128 splits (two granules per lane)
+    (40001, 700, 1, 8192, 768),    # ragged query block (a partly live wave, whole dead waves), k = 1
+    (40001, 700, 12, 8192, 384),
+    (40001, 1024, 12, 0, 768),     # no seed: compaction from the first block on
+    (33000, 2048, 8, 8192, 768),   # 32 splits
+    (33000, 4096, 10, 8192, 384),  # 16 splits: several first-round queries per wave, no later rounds
+    (5000, 600, 10, 0, 768),
+    (5000, 600, 10, 8192, 768),    # 157 blocks over 80 splits: too few for self-seeding
+    (300, 512, 5, 0, 768),         # 10 row blocks over 8 splits, queries 300.. of the second block dead
 ])
-def test_qres_matches_tilelane(cuda, dtype, n, B, k, sample):
+def test_qres_matches_tilelane(cuda, dtype, n, B, k, sample, d):
     from ah_rag.embeddings import DenseIndex
-    rng = np.random.default_rng(501 + n + B + k + sample)
-    C = _clustered(rng, n, 768)
-    Q = _clustered(rng, B, 768)
-    ix = DenseIndex(768, n, dtype=dtype, device=cuda)
+    rng = np.random.default_rng(501 + n + B + k + sample + d)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype=dtype, device=cuda)
     ix.upsert(C)
     ix.set_sample_rows(sample)
     a = _check_forms(ix, Q, k)
@@ -102,8 +102,12 @@ def test_qres_default_plan(cuda):
     ix.upsert(np.zeros((20000, 768), np.float32))
     assert ix.plan(1024, 10)["kernel"] == "tilelane128"
     ix.close()
-    ix = DenseIndex(384, 90000, dtype="bf16", device=cuda)  # not the resident dimension
+    ix = DenseIndex(384, 90000, dtype="bf16", device=cuda)  # the other resident dimension
     ix.upsert(np.zeros((90000, 384), np.float32))
+    assert ix.plan(1024, 10)["kernel"] == "qres256"
+    ix.close()
+    ix = DenseIndex(512, 90000, dtype="bf16", device=cuda)  # not a resident dimension
+    ix.upsert(np.zeros((90000, 512), np.float32))
     assert ix.plan(1024, 10)["kernel"] != "qres256"
     ix.close()
     ix = DenseIndex(768, 90000, dtype="f32", device=cuda)  # exact mode keeps the fp32 tile kernel
@@ -112,16 +116,27 @@ def test_qres_default_plan(cuda):
     ix.close()
 
 
-@pytest.mark.parametrize("sample,k", [(8192, 10), (0, 10), (0, 12)])
-def test_qres_adversarial_order(cuda, sample, k):
-    """Rows sorted so that every row beats the ones before it for query 0 (each row a new record of
-    that lane: the buffer fills and compacts again and again) and the seed is drawn from the worst
-    rows; other queries see the same rows in clustered order."""
+@pytest.mark.parametrize("sample,k,order", [(8192, 10, "asc"), (0, 10, "asc"), (0, 12, "asc"), (8192, 12, "desc"),
+                                            (8192, 10, "split")])
+def test_qres_adversarial_order(cuda, sample, k, order):
+    """asc: rows sorted so that every row beats the ones before it for query 0 (each row a new
+    record of that lane: the buffer fills and compacts again and again; every published maximum is
+    low until the last split's); desc: the best rows first (block 0 of split 0 holds the top k, the
+    first seed is exactly the k-th score: ties with the threshold); split: query 0's 64 best rows
+    all inside the last split. Other queries see the same rows in clustered order."""
     from ah_rag.embeddings import DenseIndex
-    rng = np.random.default_rng(61 + sample)
+    rng = np.random.default_rng(61 + sample + k)
     C = _clustered(rng, 40000, 768)
     Q = _clustered(rng, 1024, 768)
-    C = C[np.argsort(C @ Q[0])]
+    s0 = C @ Q[0]
+    if order == "asc":
+        C = C[np.argsort(s0)]
+    elif order == "desc":
+        C = C[np.argsort(-s0)]
+    else:
+        top = np.argsort(-s0)[:64]
+        rest = np.setdiff1d(np.arange(len(C)), top)
+        C = np.concatenate([C[rest], C[top]])
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     ix.set_sample_rows(sample)
@@ -138,7 +153,7 @@ def test_qres_ties_order_by_row(cuda):
     pick = rng.integers(0, 300, 600)
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
-    for flags, k in ((QRES, 10), (QRES, 12), (QRES | QRES_BLK, 12), (QRES | QRES16, 10), (QRES | QRES4W, 10)):
+    for flags, k in ((QRES, 10), (QRES, 12), (QRES | PREPASS, 12)):
         s, r = _run(ix, base[pick], k, flags, "qres256")
         np.testing.assert_array_equal(r, pick[:, None] + 300 * np.arange(k)[None, :])
         assert (s == s[:, :1]).all()
@@ -211,12 +226,54 @@ def test_qres_query_conversion_paths(cuda, dim, normalize):
     ix = DenseIndex(dim, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     outs = []
-    for flags, kernel in ((QRES, "qres256"), (QRES | QRES16, "qres256"), (QRES | QRES4W, "qres256"), (T256, "t256"),
-                          (TILELANE, "tilelane128")):
+    for flags, kernel in ((QRES, "qres256"), (TILELANE, "tilelane128")):
         ix.set_debug_flags(flags)
         assert ix.plan(len(Q), 10)["kernel"] == kernel
         outs.append([t.cpu().numpy() for t in ix.query(Q, 10, normalize=normalize)])
     ix.close()
-    for a, b in ((outs[0], outs[3]), (outs[1], outs[2])):
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+
+
+def test_qres_consecutive_launches(cuda):
+    """Back-to-back self-seeded launches on one workspace with changing batch sizes (so the split
+    count, and the granule layout, change between launches) and k: every launch equals the tile
+    kernel. Granules left by an earlier launch carry its epoch and must not seed this one."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(37)
+    C = _clustered(rng, 60000, 768)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    shapes = [(1024, 10), (512, 10), (2048, 12), (700, 1), (1024, 10), (600, 8)]
+    Qs = [_clustered(rng, B, 768) for B, _ in shapes]
+    ix.set_debug_flags(QRES)
+    got = [[t.cpu().numpy() for t in ix.query(Q, k)] for Q, (_, k) in zip(Qs, shapes)]
+    ix.set_debug_flags(TILELANE)
+    for Q, (_, k), a in zip(Qs, shapes, got):
+        b = [t.cpu().numpy() for t in ix.query(Q, k)]
         np.testing.assert_array_equal(a[1], b[1])
         np.testing.assert_array_equal(a[0], b[0])
+    ix.close()
+
+
+def test_qres_reserve_allocates_nothing(cuda):
+    """After reserve() the self-seeded plan's query calls allocate nothing (graph-capturable): the
+    fragment-major query copy and the seeding granules are sized by reserve."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(43)
+    C = _clustered(rng, 40000, 768)
+    Q = torch.from_numpy(_clustered(rng, 1024, 768)).to(cuda)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ix.reserve(1024, 12)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(device=cuda)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out = ix.query(Q, 10, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    ref = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    np.testing.assert_array_equal(out[1].cpu().numpy(), ref[1])
+    np.testing.assert_array_equal(out[0].cpu().numpy(), ref[0])
+    ix.close()

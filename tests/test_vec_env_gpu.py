@@ -17,9 +17,9 @@ def _norm(x):
     return json.loads(json.dumps(x, default=lambda o: o.tolist() if hasattr(o, "tolist") else str(o)))
 
 
-def test_vec_env_matches_reference_episodes(tmp_path, cuda):
-    os.environ["AHR_ENCODER"] = "hash"
-    os.environ["AHR_INDEX_DTYPE"] = "f32"
+def test_vec_env_matches_reference_episodes(tmp_path, cuda, monkeypatch):
+    monkeypatch.setenv("AHR_ENCODER", "hash")
+    monkeypatch.setenv("AHR_INDEX_DTYPE", "f32")
     from ah_rag.agent.vec_env import VecAHRAGGymEnv
     from ah_rag.graph.hierarchical_graph import HierarchicalGraph
     with open(os.path.join(GOLDEN, "gym_cases.json")) as f:

@@ -37,19 +37,13 @@ def random_actions(rng, masks):
     return [int(rng.choice(np.flatnonzero(np.asarray(m)))) for m in masks]
 
 
-def run(a) -> None:
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
-    if world > 1:
-        # replicas (SURVEY §8e C5): no collective on the data path, only the timing reduction
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-    envs = a.envs // world + (1 if rank < a.envs % world else 0)  # environments partitioned over ranks
+def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: int = 1, total_envs=None,
+            backend: str = "nccl") -> dict:
+    """One rank's C5 measurement: build the graph, then a batched VecAHRAGGymEnv episode of `envs`
+    environments (reset + `steps` steps of random valid actions) and, on rank 0, `single`
+    environments stepped one by one. Returns the result dict (the job time is the slowest rank's
+    when world > 1: an all-reduce of the episode time, the only collective)."""
+    total_envs = envs if total_envs is None else total_envs
     rng = np.random.default_rng(20251003 + rank)
     t0 = time.perf_counter()
     corpus = SyntheticCorpus(HOTPOT_90K, dev)
@@ -67,17 +61,17 @@ def run(a) -> None:
         if world > 1:
             dist.barrier()
 
-    venv = VecAHRAGGymEnv(n_envs=envs, max_steps=a.steps + 1, graph=hg)
+    venv = VecAHRAGGymEnv(n_envs=envs, max_steps=steps + 1, graph=hg)
     # warm-up episode: device graph, index, expansion kernels, host caches
     venv.reset(queries, query_vectors=qv)
-    for _ in range(a.steps):
+    for _ in range(steps):
         venv.step(random_actions(rng, [e.get_action_mask() for e in venv.envs]))
     barrier()
     t1 = time.perf_counter()
     venv.reset(queries, query_vectors=qv)
     t_reset = time.perf_counter() - t1
     step_times = []
-    for _ in range(a.steps):
+    for _ in range(steps):
         masks = [e.get_action_mask() for e in venv.envs]
         acts = random_actions(rng, masks)
         ts = time.perf_counter()
@@ -86,16 +80,16 @@ def run(a) -> None:
     barrier()
     vec_time = time.perf_counter() - t1
     if world > 1:  # job time = the slowest rank
-        t = torch.tensor([vec_time], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        t = torch.tensor([vec_time], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         vec_time = float(t.item())
-    vec_steps = a.envs * (1 + a.steps)  # all ranks' environments
+    vec_steps = total_envs * (1 + steps)  # all ranks' environments
 
-    single = None
-    if rank == 0 and a.single > 0:
+    single_rate = None
+    if rank == 0 and single > 0:
         # single-environment loop (B = 1 per search / expansion), a subset of the same queries
-        n1 = min(a.single, envs)
-        env = AHRAGGymEnv(max_steps=a.steps + 1, graph=hg)
+        n1 = min(single, envs)
+        env = AHRAGGymEnv(max_steps=steps + 1, graph=hg)
         env.env.logging_enabled = False
         hg.search_batch(queries[:1], top_k=5, return_cluster=True, query_vectors=qv[:1])
         ts = time.perf_counter()
@@ -104,21 +98,38 @@ def run(a) -> None:
             sub = VecAHRAGGymEnv.__new__(VecAHRAGGymEnv)
             sub.hg, sub.envs = hg, [env]
             sub.reset([queries[i]], query_vectors=qv[i:i + 1])
-            for _ in range(a.steps):
+            for _ in range(steps):
                 env.step(random_actions(rng, [env.get_action_mask()])[0])
-        single = round(n1 * (1 + a.steps) / (time.perf_counter() - ts), 1)
+        single_rate = round(n1 * (1 + steps) / (time.perf_counter() - ts), 1)
+    return {
+        "metric": f"env steps/sec (reset + steps, 2-hop expand + rerank), C5 on {world} MI355X",
+        "n_gpus": world, "envs": total_envs, "envs_per_gpu": envs, "steps_per_episode": steps,
+        "vec_env_steps_per_s": round(vec_steps / vec_time, 1),
+        "episode_s": round(vec_time, 4),
+        "vec_step_only_per_s_rank0": round(envs * steps / sum(step_times), 1),
+        "vec_reset_ms_rank0": round(t_reset * 1e3, 2), "vec_step_ms_rank0": [round(t * 1e3, 2) for t in step_times],
+        "single_env_steps_per_s": single_rate,
+        "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
+        "build_s": round(t_build, 1), "parallelism": f"replicas{world} (environments partitioned, no collective)",
+        "data": "synthetic HotpotQA-distractor-shaped graph (SURVEY §8d), seeded corpus vectors, random valid actions",
+    }
+
+
+def run(a) -> None:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        # replicas (SURVEY §8e C5): no collective on the data path, only the timing reduction
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    envs = a.envs // world + (1 if rank < a.envs % world else 0)  # environments partitioned over ranks
+    out = measure(dev, envs, a.steps, a.single, rank, world, a.envs, a.backend)
     if rank == 0:
-        out = {
-            "metric": f"env steps/sec (reset + steps, 2-hop expand + rerank), C5 on {world} MI355X",
-            "n_gpus": world, "envs": a.envs, "envs_per_gpu": envs, "steps_per_episode": a.steps,
-            "vec_env_steps_per_s": round(vec_steps / vec_time, 1),
-            "vec_step_only_per_s_rank0": round(envs * a.steps / sum(step_times), 1),
-            "vec_reset_ms_rank0": round(t_reset * 1e3, 2), "vec_step_ms_rank0": [round(t * 1e3, 2) for t in step_times],
-            "single_env_steps_per_s": single,
-            "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
-            "build_s": round(t_build, 1), "parallelism": f"replicas{world} (environments partitioned, no collective)",
-            "data": "synthetic HotpotQA-distractor-shaped graph (SURVEY §8d), seeded corpus vectors, random valid actions",
-        }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
