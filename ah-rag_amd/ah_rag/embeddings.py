@@ -334,7 +334,8 @@ class DenseIndex:
         16x16x32 kernel (bf16/f16, k <= 16), 131072 / 262144 = always / never the k-blocked kernel,
         1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
         1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768,
-        k <= 12), 1 << 26 = that kernel seeded by the sampled pre-pass instead of seeding itself.
+        k <= 12), 1 << 26 = that kernel seeded by the sampled pre-pass instead of seeding itself, 1 << 27 = its
+        self-seeding with the first event only.
         Garbage-result cost-split switches (2, 256, 512, 1024, 1 << 20, 1 << 21, 1 << 24, 1 << 25)
         need the ablation build."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags) & 0xFFFFFFFF), "ahr_index_set_debug_flags")

@@ -3257,6 +3257,25 @@ int ensure_ss(ahr_index* ix, hipStream_t s) {
   return AHR_OK;
 }
 
+// The register-resident kernel's self-seeding schedule over a split's block index: publications
+// after blocks 0, 2, 6, 14, 30 and seeding events at the ends of blocks 1 (the first, waiting), 3,
+// 7, 15, 31 — each event's selection uses the maxima of the publication one block before it, so
+// the seed tightens from a 2-block-per-split sample to a 31-block one as the splits advance.
+// AHR_QRES_PUB / AHR_QRES_EV (hex bit masks) override it for tuning.
+struct QresSchedule {
+  uint64_t pub, ev;
+};
+inline QresSchedule qres_schedule() {
+  static const QresSchedule sch = [] {
+    QresSchedule d{(1ull << 0) | (1ull << 2) | (1ull << 6) | (1ull << 14) | (1ull << 30),
+                   (1ull << 3) | (1ull << 7) | (1ull << 15) | (1ull << 31)};
+    if (const char* e = getenv("AHR_QRES_PUB")) d.pub = strtoull(e, nullptr, 16);
+    if (const char* e = getenv("AHR_QRES_EV")) d.ev = strtoull(e, nullptr, 16);
+    return d;
+  }();
+  return sch;
+}
+
 // the second query buffer (the register-resident plan's fragment-major copy, or the k-blocked
 // copy of the kb256 plan), zeroed on the caller's stream when allocated
 int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
@@ -3626,14 +3645,12 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const uint32_t flags = (p.xcd_remap ? kFlagXcdRemap : 0u) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
     if (p.kernel == KERNEL_QRES) {
-      uint64_t* pub = nullptr;
-      uint64_t* seeds = nullptr;
-      if (self_seed) {  // tag, [q_cap][n_splits] maxima, [q_cap] seeds
-        pub = ix->ss + 1;
-        seeds = pub + ix->q_cap * (int64_t)p.n_splits;
-      }
+      // self-seeding buffer: the tag (ss[0]), then [256 qblocks][n_splits] maxima and [256 qblocks] seeds
+      const QresSchedule sch = qres_schedule();
+      const bool once = (flags & kFlagQresSeedOnce) != 0;
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
-                   p.n_splits, p.qblocks, (int)flags, pub, seeds, reinterpret_cast<const uint32_t*>(ix->ss), s);
+                   p.n_splits, p.qblocks, (int)flags, self_seed ? ix->ss + 1 : nullptr, once ? 1 : sch.pub,
+                   once ? 0 : sch.ev, s);
       return;
     }
     if (p.kernel == KERNEL_KB256) {

@@ -193,7 +193,7 @@ enum : uint32_t {
   kFlagNoBarrier = 1u << 24,  // qres kernel: no stage barriers (wrong results)
   kFlagNoLdsRead = 1u << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
   kFlagQresPrepass = 1u << 26,   // qres kernel seeded by the sampled pre-pass launch, not by itself (A/B)
-  kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first round only (A/B)
+  kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first event only, no later rounds (A/B)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in

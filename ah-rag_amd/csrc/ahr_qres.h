@@ -26,12 +26,15 @@ void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes
 
 // One fused launch: part_keys [B][n_splits][k] (the merge kernels' input), thr [B] optional
 // admission seeds. grid = n_splits * qblocks; n_splits % 8 == 0 when flags has the XCD remap bit.
-// pub [q_pad][n_splits] / seeds [q_pad] (q_pad = 256 * qblocks rounded up to the workspace): the
-// self-seeding granules, nullptr for none; *epoch: the launch's tag, which the query conversion
-// stream-ordered before this launch advanced (no earlier launch on these buffers used it).
+// pub: the self-seeding buffer, nullptr for none: pub[-1] = the launch's tag (low 32 bits), which
+// the query conversion stream-ordered before this launch advanced (no earlier launch on these
+// buffers used it); then [256 qblocks][n_splits] published maxima, then [256 qblocks] seeds.
+// pub_mask / ev_mask: the self-seeding schedule over a split's block index (bit bi: publish the
+// running maxima after block bi / a seeding event at the end of block bi; block 0's publication and
+// the first event at block 1 are always there).
 void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int d_pad_bytes,
             int n_rows, int B, uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks,
-            int flags, uint64_t* pub, uint64_t* seeds, const uint32_t* epoch, hipStream_t s);
+            int flags, uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s);
 
 }  // namespace qres
 }  // namespace dense

@@ -57,23 +57,28 @@ struct Cfg {
   static constexpr int kPPW = kPieces / kWaves;   // pieces per wave per stage
   static constexpr int kNS = NKT * 4;             // k16 steps = query fragments per lane
   static constexpr int kSS = kSK * 4;             // k16 steps per stage
-  // LDS: the ring, the seeding scratch (per wave 3 KiB: the tail of the first seed's parked
-  // accumulators, a round's selection granules, a round's seed granules), the lane buffers
+  // LDS: the ring, the seeding scratch (per wave 1 KiB: the tail of a seeding event's parked
+  // accumulators), the lane buffers
   static constexpr int kOffSeed = kSlots * kStage;
-  static constexpr int kSeedBytes = kWaves * 3 * 1024;
+  static constexpr int kSeedBytes = kWaves * 1024;
   static constexpr int kOffBuf = kOffSeed + kSeedBytes;
   static constexpr int kLds = kOffBuf + kBufCap * kThreads * 8;
 };
 static_assert(Cfg<12>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
 
-// Self-seeding schedule over a split's block index bi (uniform): publish the running maxima after
-// block 0, 3, 7, 15, ...; the first seed is selected and read at the end of block 1 (bounded
-// waits); later rounds select D blocks after their publication and read D blocks after that (D =
-// 1 at two stages per block, 2 at one: the granules travel by LDS-DMA issued one stage ahead).
-__device__ __forceinline__ bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
-__device__ __forceinline__ bool ss_pub(int bi) { return bi == 0 || (bi >= 3 && pow2(bi + 1)); }
-__device__ __forceinline__ bool ss_round(int bi) { return bi >= 3 && pow2(bi + 1); }
+// Self-seeding schedule (uniform, over a split's block index bi < 64; the host passes it): after
+// block bi with bit bi of pub_mask set, a split publishes its running per-query maxima; at the end
+// of block bi with bit bi of ev_mask set, a seeding event: the selecting splits take the k-th
+// largest published maxima as seeds, every split reads its queries' seeds. The first event (block
+// 1, after the block-0 publication) waits, bounded, for every granule and seed; later events use
+// what is there (an earlier round's granule is still a valid lower bound), so they never wait.
+// From block 64 on (large corpora) the schedule continues geometrically: a publication after block
+// 2^m - 2 and an event at the end of block 2^m - 1.
 constexpr uint32_t kSeedWaitTicks = 3000;  // s_memrealtime ticks (100 MHz): a 30-us bound per wait
+__device__ __forceinline__ bool pow2(int x) { return (x & (x - 1)) == 0; }
+__device__ __forceinline__ bool in_sched(uint64_t mask, int bi, int off) {
+  return bi < 64 ? ((mask >> bi) & 1) != 0 : pow2(bi + off);
+}
 
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
@@ -116,15 +121,6 @@ __device__ __forceinline__ uint64_t granule_load(const uint64_t* p) {
 __device__ __forceinline__ void granule_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
 }
-// 1 KiB of granules (64 lanes x 16 B from base; bytes past `bytes` read as 0) into LDS by an sc1
-// LDS-DMA: no registers held while it is in flight, and it retires in order with the ring's DMA
-__device__ __forceinline__ void granules_to_lds(const uint64_t* base, uint32_t bytes, unsigned char* lds, int lane) {
-  const __amdgpu_buffer_rsrc_t r = tile_rsrc_u(base, bytes);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (uint32_t)lane * 16,
-                                           0, 0, 16 /* sc1 */);
-}
-
-
 __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ qbuf, int64_t row_stride, int64_t n16,
                                                    int ns, uint8_t* __restrict__ qfrag, uint32_t* __restrict__ epoch) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 16-B chunk of the output
@@ -139,16 +135,15 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
 }
 
 
-// pub [q_pad][n_splits] and seeds [q_pad]: the self-seeding granules (nullptr: no self-seeding;
-// thr_init, if any, is the admission threshold). *epoch_p: this launch's tag, advanced on the
-// device by the query conversion launched before it (so a replayed hipGraph gets a fresh one).
-// ROUNDS: the later self-seeding rounds compiled in (the first round is always there).
-template <int DT, int NKT, int KCAP, int ABL, bool ROUNDS>
+// pub: the self-seeding buffer (nullptr: no self-seeding; thr_init, if any, is the admission
+// threshold): pub[-1] holds this launch's tag (low 32 bits), advanced on the device by the query
+// conversion launched before it, so a replayed hipGraph gets a fresh one; then [256 qblocks]
+// [n_splits] published maxima, then [256 qblocks] seeds.
+template <int DT, int NKT, int KCAP, int ABL>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
-    int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t* __restrict__ seeds,
-    const uint32_t* __restrict__ epoch_p) {
+    int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t pub_mask, uint64_t ev_mask) {
   using C = Cfg<NKT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -177,12 +172,10 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   const int q = qw0 + fr;
   // self-seeding needs every split's first two blocks and at most 128 splits (grid-uniform)
   const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && n_blocks >= 2 * n_splits && n_splits <= 128;
-  // later rounds: at most one selected query per wave (n_splits >= 32)
-  const bool ss_rounds = ROUNDS && ss && n_splits >= 32;
-  constexpr int kD = C::kSPB == 1 ? 2 : 1;  // blocks from a round's publication to its selection
 
   float thr = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
-  const uint32_t epoch = pub ? *epoch_p : 0u;
+  const uint32_t epoch = pub ? (uint32_t)pub[-1] : 0u;
+  uint64_t* const seeds = pub + (int64_t)qblocks * kTQ * n_splits;
 
   // DMA: piece p = wave + 8 i of a stage is k-tile p / 4, rows 8 (p % 4) .. +8; lane l lands at
   // (row 8 (p % 4) + l / 8, physical chunk l % 8) and loads logical chunk (l % 8) ^ swz(row)
@@ -232,9 +225,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     asm volatile("" : "+v"(t));
     return lbuf0 + t;
   };
-  // this wave's seeding scratch: [0, 1 KiB) parked accumulator tail, [1, 2) selection granules,
-  // [2, 3) seed granules
-  unsigned char* const wscr = smem + C::kOffSeed + wave * 3 * 1024;
+  // this wave's seeding scratch: a seeding event's parked accumulator tail (1 KiB)
+  unsigned char* const wscr = smem + C::kOffSeed + wave * 1024;
   int nb = 0;
   // keep the k_out best buffered keys; the smallest kept is the lane's k-th best: new threshold
   auto compact = [&]() {
@@ -314,15 +306,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     asm volatile("" : "+v"(qq));
     if (!fh && qq < n_q) granule_store(pub + (int64_t)qq * n_splits + split, ((uint64_t)epoch << 32) | ord_f32(pm));
   };
-  // the query this wave selects in the later rounds (slot j of the query block, j mod n_splits ==
-  // split, in this wave's 32; n_splits >= 32: at most one), -1 for none. Uniform.
-  auto sel_query = [&]() __attribute__((always_inline)) {
-    const int j = wave * 32 + (((split - wave * 32) % n_splits) + n_splits) % n_splits;
-    const int64_t qq = (int64_t)qb * kTQ + j;
-    return (j < wave * 32 + 32 && qq < n_q) ? qq : (int64_t)-1;
-  };
-  // The first round: every query j of this wave with j mod n_splits == split, polling (bounded)
-  // until every split's granule is there; the k-th largest published maximum becomes its seed.
+  // A seeding event: every query j of this wave with j mod n_splits == split, polling (bounded) until
+  // every split's granule of this launch is there (after the first event they all are); the k-th
+  // largest published maximum becomes its seed.
   auto select_wait = [&]() __attribute__((always_inline)) {
     const int j0 = wave * 32 + (((split - wave * 32) % n_splits) + n_splits) % n_splits;
 #pragma unroll 1
@@ -353,7 +339,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (q < n_q && (uint32_t)(g >> 32) == epoch && (uint32_t)g != 0)
       thr = fmaxf(thr, key_score((uint64_t)(uint32_t)g << 32));
   };
-  auto read_wait = [&]() __attribute__((always_inline)) {  // the first round: poll (bounded) for the seeds
+  auto read_wait = [&]() __attribute__((always_inline)) {  // poll (bounded) until this launch's seeds are there
     uint64_t g = 0;
     int qq = q;
     asm volatile("" : "+v"(qq));
@@ -366,32 +352,6 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       __builtin_amdgcn_s_sleep(2);
     }
     apply_seed(g);
-  };
-  // later rounds: the granules come into the wave's scratch by LDS-DMA one stage before their use
-  auto sel_fetch = [&](int64_t qq) __attribute__((always_inline)) {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    granules_to_lds(pub + qq * n_splits, (uint32_t)n_splits * 8, wscr + 1024, ln);
-  };
-  auto sel_use = [&](int64_t qq) __attribute__((always_inline)) {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint64_t* g = reinterpret_cast<const uint64_t*>(wscr + 1024);
-    const uint64_t g0 = g[ln], g1 = g[ln + 64];  // past n_splits: zeros
-    const uint32_t v0 = (uint32_t)(g0 >> 32) == epoch ? (uint32_t)g0 : 0u;
-    const uint32_t v1 = (uint32_t)(g1 >> 32) == epoch ? (uint32_t)g1 : 0u;
-    const uint32_t m = wave_kth(v0, v1, k_out, lane);
-    if (m != 0 && lane == 0) granule_store(seeds + qq, ((uint64_t)epoch << 32) | m);
-  };
-  auto read_fetch = [&]() __attribute__((always_inline)) {  // the wave's 32 seeds (256 B)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    granules_to_lds(seeds + qw0, 256, wscr + 2048, ln);
-  };
-  auto read_use = [&]() __attribute__((always_inline)) {
-    int f = fr;
-    asm volatile("" : "+v"(f));
-    apply_seed(reinterpret_cast<const uint64_t*>(wscr + 2048)[f]);
   };
   // block 0's raw scores parked in the upper half of the lane buffer (entries 8 .. 15, two floats
   // each) until the first seed; replayed quad by quad from the bottom while the appends fill the
@@ -462,13 +422,13 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto finish_block = [&](int bi, int64_t sq) __attribute__((always_inline)) {  // bi: the block just multiplied
+  auto finish_block = [&](int bi) __attribute__((always_inline)) {  // bi: the block just multiplied
     if constexpr (skip_screen) {  // GEMM only: the chain kept live (rule 17), no top-k
       asm volatile("" ::"v"(acc));
       return;
     }
     const int r0 = (b_begin + bi) * kTR;
-    if (ss && bi == 0) {  // the first round's sample: park the scores, publish the maxima
+    if (ss && bi == 0) {  // the first event's sample: park the scores, publish the maxima
       park(acc);
 #pragma unroll
       for (int j = 0; j < 16; ++j)  // block 0 is never ragged (>= 2 blocks per split) but check anyway
@@ -477,17 +437,13 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       return;
     }
     screen_quads(acc, r0);
-    if (ss_rounds) {
-      if (ss_round(bi)) publish();
-      if (sq >= 0) sel_use(sq);
-      if (bi >= 2 * kD && ss_round(bi - 2 * kD)) read_use();
-    }
+    if (ss && in_sched(pub_mask, bi, 2)) publish();
   };
-  // The first seed (bounded waits) at the end of block 1, before the block's screening: its 16
-  // accumulators wait in LDS (12 in the ring slot that is free then — stage j - 1's, whose refill
-  // is issued only after this path — and 4 in the wave's scratch), so the waits and the replay of
-  // block 0 hold no accumulator registers; the main loop has none to spare.
-  auto first_seed = [&](int j) __attribute__((always_inline)) {
+  // A seeding event at the end of a block, before its screening: the block's 16 accumulators wait
+  // in LDS (12 in the ring slot that is free then — stage j - 1's, whose refill is issued only
+  // after this path — and 4 in the wave's scratch), so the waits (and, at the first event, the
+  // replay of block 0) hold no accumulator registers; the main loop has none to spare.
+  auto seed_event = [&](int j, bool first) __attribute__((always_inline)) {
     float* const pa = reinterpret_cast<float*>(slot_of(j - 1)) + tid * 4;
     float* const pb = reinterpret_cast<float*>(wscr) + lane * 4;
     auto at = [&](int i) __attribute__((always_inline)) { return i < 12 ? pa + (i >> 2) * kThreads * 4 : pb; };
@@ -496,7 +452,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     asm volatile("" ::: "memory");
     select_wait();
     read_wait();
-    replay(b_begin * kTR);
+    if (first) replay(b_begin * kTR);
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 16; i += 4) {
@@ -510,21 +466,12 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 #pragma unroll 1
   for (int j = 0; j <= n_st; ++j) {
     stage_sync(j);
-    const bool seed_now = ss && j == 2 * C::kSPB;  // uniform
     const bool bend = j >= C::kSPB && j % C::kSPB == 0;  // block j / kSPB - 1 ended with stage j - 1
-    // this round's granules go to LDS at the last stage sync of the block that uses them (before
-    // the stage's DMA: the next sync's counted wait covers them)
-    int64_t sq = -1;
-    if (ss_rounds && live && (j + 1) % C::kSPB == 0 && j + 1 >= C::kSPB) {
-      const int bu = (j + 1) / C::kSPB - 1;  // the block whose end uses them
-      if (bu >= kD && ss_round(bu - kD)) {
-        sq = sel_query();
-        if (sq >= 0) sel_fetch(sq);
-      }
-      if (bu >= 2 * kD && ss_round(bu - 2 * kD)) read_fetch();
-    }
-    if (seed_now) {
-      if (live) first_seed(j);
+    const int bi = j / C::kSPB - 1;
+    const bool first = ss && j == 2 * C::kSPB;  // uniform
+    const bool event = first || (ss && bend && in_sched(ev_mask, bi, 1));
+    if (event) {
+      if (live) seed_event(j, first);
       lds_barrier();  // every wave's parked accumulators are back before the slot is refilled
     }
     if (j + 2 < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + 2);
@@ -534,10 +481,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       fa[0] = frag(j, 0);
       fa[1] = frag(j, 1);
     }
-    if (bend) {
-      const int bi = j / C::kSPB - 1;
-      finish_block(bi, (ss_rounds && bi >= kD && ss_round(bi - kD)) ? sel_query() : (int64_t)-1);
-    }
+    if (bend) finish_block(bi);
     if (mma) {
       if (C::kSPB == 1 || !(j & 1))
         stage_mma(std::integral_constant<int, 0>{}, j);
@@ -588,59 +532,61 @@ void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes
                      qfrag, epoch);
 }
 
-template <int DT, int NKT, int KCAP, int ABL = 0, bool ROUNDS = false>
+template <int DT, int NKT, int KCAP, int ABL = 0>
 void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, uint64_t* pub,
-              uint64_t* seeds, const uint32_t* epoch, hipStream_t s) {
+              uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
   if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
     const int abl = ((flags & kFlagSkipEpilogue) ? ABL_NOSCREEN : 0) | ((flags & kFlagNoLoads) ? ABL_NOLOADS : 0) |
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
                     ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0);
 #define AHR_QRES_ABL(V) \
-  case V: launch_t<DT, NKT, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, seeds, epoch, s); return;
+  case V: launch_t<DT, NKT, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       default: break;
     }
 #undef AHR_QRES_ABL
   }
-  constexpr auto kern = &topk_qres_kernel<DT, NKT, KCAP, ABL, ROUNDS>;
+  constexpr auto kern = &topk_qres_kernel<DT, NKT, KCAP, ABL>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), Cfg<NKT>::kLds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), Cfg<NKT>::kLds, s, rows, qfrag,
-                     row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, seeds, epoch);
+                     row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask,
+                     ev_mask);
 }
 
 template <int DT, int NKT>
 void launch_k(int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
               uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
-              uint64_t* pub, uint64_t* seeds, const uint32_t* epoch, hipStream_t s) {
+              uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
   if (k <= 8)
     launch_t<DT, NKT, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub,
-                         seeds, epoch, s);
+                         pub_mask, ev_mask, s);
   else
     launch_t<DT, NKT, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags,
-                          pub, seeds, epoch, s);
+                          pub, pub_mask, ev_mask, s);
 }
 
 void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int d_pad_bytes,
             int n_rows, int B, uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks,
-            int flags, uint64_t* pub, uint64_t* seeds, const uint32_t* epoch, hipStream_t s) {
+            int flags, uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
   const bool wide = d_pad_bytes == 12 * kRowBytes;
+  pub_mask |= 1;  // block 0's maxima: the first event's sample
   if (dtype == AHR_BF16) {
     if (wide)
       launch_k<DT_BF16, 12>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                            pub, seeds, epoch, s);
+                            pub, pub_mask, ev_mask, s);
     else
       launch_k<DT_BF16, 6>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                           pub, seeds, epoch, s);
+                           pub, pub_mask, ev_mask, s);
   } else {
     if (wide)
       launch_k<DT_F16, 12>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                           pub, seeds, epoch, s);
+                           pub, pub_mask, ev_mask, s);
     else
       launch_k<DT_F16, 6>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                          pub, seeds, epoch, s);
+                          pub, pub_mask, ev_mask, s);
   }
 }
 

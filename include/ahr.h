@@ -133,7 +133,7 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
  * launch instead of the last-workgroup fold, 1 << 23 = the 256-query register-resident kernel
  * (qres256) wherever it applies (bf16/f16, d_pad 384 or 768, k <= 12), 1 << 26 = qres256 seeded
  * by the sampled pre-pass launch instead of seeding itself, 1 << 27 = qres256's self-seeding with
- * its first round only.
+ * its first event only (no later rounds).
  * Cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
  * only, 512 = operands of the first tile only, 1024 = loads never waited for, 1048576 / 2097152 =
  * k-blocked tiles read from tile 0 / the split's first tile, 1 << 24 / 1 << 25 = qres256 without

@@ -1,0 +1,12 @@
+#!/bin/bash
+# rocprofv3 kernel trace + PMC passes (HBM bytes, MFMA busy) and their summary for one workload.
+# usage: bash tools/gpu/profile.sh OUTDIR WORKLOAD(hotpot90k|synth5m) [extra bench args]
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=$1; W=$2; shift 2
+mkdir -p $O
+if [ "$W" == "synth5m" ]; then STEPS="--steps 5 --warmup 2"; else STEPS="--steps 10 --warmup 3"; fi
+bash tools/profile_pmc.sh $O --workload $W $STEPS --no-cpu-baseline --inflight 1 --no-batch-sweep --no-f32-line --no-sublines "$@" || { echo PROFILE_FAILED; exit 1; }
+python tools/pmc_summary.py $O --workload $W --batch 1024 --out $O/pmc_traffic.json || exit 1
+cut -c1-800 $O/pmc_traffic.json

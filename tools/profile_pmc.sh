@@ -5,7 +5,7 @@ set -u
 OUT=${1:-gpurun_out/pmc}; shift || true
 # --inflight 1: per-kernel durations without the deliberate cross-batch overlap (the roofline is
 # per launch; bench.py takes it from a serial event-timed pass too)
-ARGS=${@:-"--steps 10 --warmup 3 --no-cpu-baseline --inflight 1"}
+ARGS=${@:-"--steps 10 --warmup 3 --no-cpu-baseline --inflight 1 --no-sublines"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" --output-format csv -- python -u bench.py $ARGS > "$OUT/trace.log" 2>&1 || exit $?
