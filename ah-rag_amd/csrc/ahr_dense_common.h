@@ -194,6 +194,7 @@ enum : uint32_t {
   kFlagNoLdsRead = 1u << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
   kFlagQresPrepass = 1u << 26,   // qres kernel seeded by the sampled pre-pass launch, not by itself (A/B)
   kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first event only, no later rounds (A/B)
+  kFlagQresHalfStages = 1u << 28,  // qres at d_pad 768: two 24-KiB stages per block, 3-slot ring (A/B)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
@@ -208,7 +209,7 @@ constexpr uint32_t kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
 constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
                                        kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead;
 constexpr uint32_t kKnownFlags = kKernelFlags | kWrongResultFlags | kFlagNoTilePrefetch | kFlagNoFold |
-                                 kFlagQresPrepass | kFlagQresSeedOnce;
+                                 kFlagQresPrepass | kFlagQresSeedOnce | kFlagQresHalfStages;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 }  // namespace dense

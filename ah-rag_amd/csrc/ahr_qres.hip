@@ -46,25 +46,31 @@ namespace ahr {
 namespace dense {
 namespace qres {
 
-template <int NKT>
+// NKT 64-deep k-tiles per row (12 at d_pad 768, 6 at 384), SPB stages per 32-row block: a stage is
+// NKT / SPB k-tiles (24 KiB or a whole 48-KiB block). 24-KiB stages run a 3-slot ring issued two
+// stages ahead; 48-KiB stages a 2-slot ring issued one stage (a whole block) ahead.
+template <int NKT, int SPB>
 struct Cfg {
-  static_assert(NKT % 6 == 0, "stages of 6 k-tiles");
-  static constexpr int kSK = 6;                   // k-tiles per stage
-  static constexpr int kSPB = NKT / kSK;          // stages per 32-row block
-  static constexpr int kStage = kSK * kKt;        // 24 KiB
+  static_assert(NKT % (6 * SPB) == 0, "stages of 6 or 12 k-tiles");
+  static constexpr int kSPB = SPB;                // stages per 32-row block
+  static constexpr int kSK = NKT / SPB;           // k-tiles per stage
+  static constexpr int kStage = kSK * kKt;        // 24 or 48 KiB
+  static constexpr int kSlots = kSK == 12 ? 2 : 3;
+  static constexpr int kAhead = kSlots - 1;       // stages in flight beyond the one multiplied
   static constexpr int kPieces = kSK * 4;         // 1-KiB DMA pieces per stage (8 rows x 128 B)
   static_assert(kPieces % kWaves == 0, "equal DMA share per wave");
   static constexpr int kPPW = kPieces / kWaves;   // pieces per wave per stage
   static constexpr int kNS = NKT * 4;             // k16 steps = query fragments per lane
   static constexpr int kSS = kSK * 4;             // k16 steps per stage
-  // LDS: the ring, the seeding scratch (per wave 1 KiB: the tail of a seeding event's parked
-  // accumulators), the lane buffers
+  // LDS: the ring, the seeding scratch (per wave 1 KiB: what of a seeding event's parked
+  // accumulators the free ring slot cannot hold; none with 48-KiB slots), the lane buffers
   static constexpr int kOffSeed = kSlots * kStage;
-  static constexpr int kSeedBytes = kWaves * 1024;
+  static constexpr int kSeedBytes = kStage >= 32 * 1024 ? 0 : kWaves * 1024;
   static constexpr int kOffBuf = kOffSeed + kSeedBytes;
   static constexpr int kLds = kOffBuf + kBufCap * kThreads * 8;
 };
-static_assert(Cfg<12>::kLds <= 160 * 1024, "LDS budget: one workgroup per CU");
+static_assert(Cfg<12, 2>::kLds <= 160 * 1024 && Cfg<12, 1>::kLds <= 160 * 1024 && Cfg<6, 1>::kLds <= 160 * 1024,
+              "LDS budget: one workgroup per CU");
 
 // Self-seeding schedule (uniform, over a split's block index bi < 64; the host passes it): after
 // block bi with bit bi of pub_mask set, a split publishes its running per-query maxima; at the end
@@ -139,12 +145,12 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
 // threshold): pub[-1] holds this launch's tag (low 32 bits), advanced on the device by the query
 // conversion launched before it, so a replayed hipGraph gets a fresh one; then [256 qblocks]
 // [n_splits] published maxima, then [256 qblocks] seeds.
-template <int DT, int NKT, int KCAP, int ABL>
+template <int DT, int NKT, int SPB, int KCAP, int ABL>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
     int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t pub_mask, uint64_t ev_mask) {
-  using C = Cfg<NKT>;
+  using C = Cfg<NKT, SPB>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // (the per-lane source offsets are recomputed at each issue: a few VALU per stage, and three
   // registers the main loop cannot spare)
   const uint32_t blk_bytes = (uint32_t)(kTR * row_stride);
-  auto slot_of = [&](int st) __attribute__((always_inline)) { return smem + (st % kSlots) * C::kStage; };
+  auto slot_of = [&](int st) __attribute__((always_inline)) { return smem + (st % C::kSlots) * C::kStage; };
   auto issue = [&](int st) __attribute__((always_inline)) {
     const int b = b_begin + st / C::kSPB;
     const __amdgpu_buffer_rsrc_t r =
@@ -199,8 +205,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       blds16(r, src_off, slot + (p >> 2) * kKt + (p & 3) * 1024);
     }
   };
-  if (n_st > 0) issue(0);
-  if (n_st > 1) issue(1);
+#pragma unroll
+  for (int st = 0; st < C::kAhead; ++st)
+    if (st < n_st) issue(st);
 
   // resident B fragments: step S of query q = bytes [32 S + 16 fh, +16) of its row
   u32x4 qf[C::kNS];
@@ -376,12 +383,12 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     }
   };
 
-  // Sync j: this wave's pieces of stage j landed (stage j + 1 may stay in flight), then the
-  // barrier: everyone's stage j landed, and everyone is done with stage j - 1, whose slot takes
-  // stage j + 2 (a 3-slot ring, a stage issued two intervals ahead).
+  // Sync j: this wave's pieces of stage j landed (with a 3-slot ring stage j + 1 may stay in
+  // flight), then the barrier: everyone's stage j landed, and everyone is done with stage j - 1,
+  // whose slot takes stage j + kAhead.
   auto stage_sync = [&](int j) __attribute__((always_inline)) {
     if (!(ABL & ABL_NOWAIT)) {
-      if (j + 1 < n_st)
+      if (C::kAhead == 2 && j + 1 < n_st)
         wait_vm<C::kPPW>();
       else
         wait_vm<0>();
@@ -392,14 +399,18 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // stored at physical chunk (2 (s % 4) + fh) ^ ((fr >> 1) & 7) = 2 ((s % 4) ^ h) + (fh ^ a0),
   // h = (fr >> 2) & 3, a0 = (fr >> 1) & 1. The byte offset is one v_xad_u32 per read from two
   // per-lane values (the four precomputed offsets would cost two more live registers).
-  const int a_base = fr * kRowBytes + ((fh ^ ((fr >> 1) & 1)) << 4);
-  const int a_h = ((fr >> 2) & 3) << 5;
+  // The four per-lane chunk offsets (s % 4 = m: a_row + 32 (m ^ h) + 16 (fh ^ a0)) are kept in
+  // registers, so a read costs one v_add (the slot base) and an immediate k-tile offset.
+  int a_off[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    a_off[m] = fr * kRowBytes + ((((2 * m + fh) ^ ((fr >> 1) & 7))) << 4);
+    asm volatile("" : "+v"(a_off[m]));  // materialized once, here
+  }
   auto frag = [&](int st, int s) __attribute__((always_inline)) {
     if constexpr ((ABL & ABL_NOREAD) != 0) return qf[(s + 5) % C::kNS];  // MFMA + issue only
     const unsigned char* slot = slot_of(st);
-    int hx;  // a_h ^ 32 (s % 4), per read (volatile: never hoisted or shared between reads)
-    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(hx) : "i"((s & 3) << 5), "v"(a_h));
-    return *reinterpret_cast<const u32x4*>(slot + (s >> 2) * kKt + (hx + a_base));
+    return *reinterpret_cast<const u32x4*>(slot + (s >> 2) * kKt + a_off[s & 3]);
   };
   static_assert(C::kSS % 3 == 0, "three fragment registers rotate evenly over a stage");
   constexpr bool skip_screen = (ABL & ABL_NOSCREEN) != 0;
@@ -440,13 +451,15 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (ss && in_sched(pub_mask, bi, 2)) publish();
   };
   // A seeding event at the end of a block, before its screening: the block's 16 accumulators wait
-  // in LDS (12 in the ring slot that is free then — stage j - 1's, whose refill is issued only
-  // after this path — and 4 in the wave's scratch), so the waits (and, at the first event, the
-  // replay of block 0) hold no accumulator registers; the main loop has none to spare.
+  // in LDS (in the ring slot that is free then — stage j - 1's, whose refill is issued only after
+  // this path — and, for 24-KiB slots, 4 of them in the wave's scratch), so the waits (and, at the
+  // first event, the replay of block 0) hold no accumulator registers; the main loop has none to
+  // spare.
   auto seed_event = [&](int j, bool first) __attribute__((always_inline)) {
     float* const pa = reinterpret_cast<float*>(slot_of(j - 1)) + tid * 4;
     float* const pb = reinterpret_cast<float*>(wscr) + lane * 4;
-    auto at = [&](int i) __attribute__((always_inline)) { return i < 12 ? pa + (i >> 2) * kThreads * 4 : pb; };
+    constexpr int kInSlot = C::kStage / (kThreads * 16) * 4;  // floats per lane the slot holds
+    auto at = [&](int i) __attribute__((always_inline)) { return i < kInSlot ? pa + (i >> 2) * kThreads * 4 : pb; };
 #pragma unroll
     for (int i = 0; i < 16; i += 4) *reinterpret_cast<f32x4*>(at(i)) = f32x4{acc[i], acc[i + 1], acc[i + 2], acc[i + 3]};
     asm volatile("" ::: "memory");
@@ -474,7 +487,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       if (live) seed_event(j, first);
       lds_barrier();  // every wave's parked accumulators are back before the slot is refilled
     }
-    if (j + 2 < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + 2);
+    if (j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + C::kAhead);
     if (!live) continue;
     const bool mma = j < n_st;
     if (mma) {  // the stage's first fragments: in flight under the screening below
@@ -532,7 +545,7 @@ void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes
                      qfrag, epoch);
 }
 
-template <int DT, int NKT, int KCAP, int ABL = 0>
+template <int DT, int NKT, int SPB, int KCAP, int ABL = 0>
 void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, uint64_t* pub,
               uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
@@ -541,53 +554,59 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
                     ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0);
 #define AHR_QRES_ABL(V) \
-  case V: launch_t<DT, NKT, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
+  case V: launch_t<DT, NKT, SPB, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       default: break;
     }
 #undef AHR_QRES_ABL
   }
-  constexpr auto kern = &topk_qres_kernel<DT, NKT, KCAP, ABL>;
+  constexpr auto kern = &topk_qres_kernel<DT, NKT, SPB, KCAP, ABL>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), Cfg<NKT>::kLds);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), Cfg<NKT>::kLds, s, rows, qfrag,
+  constexpr int lds = Cfg<NKT, SPB>::kLds;
+  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), lds, s, rows, qfrag,
                      row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask,
                      ev_mask);
 }
 
-template <int DT, int NKT>
+template <int DT, int NKT, int SPB>
 void launch_k(int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
               uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
               uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
   if (k <= 8)
-    launch_t<DT, NKT, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub,
-                         pub_mask, ev_mask, s);
+    launch_t<DT, NKT, SPB, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags,
+                              pub, pub_mask, ev_mask, s);
   else
-    launch_t<DT, NKT, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags,
-                          pub, pub_mask, ev_mask, s);
+    launch_t<DT, NKT, SPB, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks,
+                               flags, pub, pub_mask, ev_mask, s);
 }
 
 void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int d_pad_bytes,
             int n_rows, int B, uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks,
             int flags, uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
   const bool wide = d_pad_bytes == 12 * kRowBytes;
+  const bool half = (flags & kFlagQresHalfStages) != 0;  // d_pad 768: two 24-KiB stages per block
   pub_mask |= 1;  // block 0's maxima: the first event's sample
+#define AHR_QRES_L(D, N, S) \
+  launch_k<D, N, S>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags, pub, \
+                    pub_mask, ev_mask, s)
   if (dtype == AHR_BF16) {
-    if (wide)
-      launch_k<DT_BF16, 12>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                            pub, pub_mask, ev_mask, s);
+    if (wide && half)
+      AHR_QRES_L(DT_BF16, 12, 2);
+    else if (wide)
+      AHR_QRES_L(DT_BF16, 12, 1);
     else
-      launch_k<DT_BF16, 6>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                           pub, pub_mask, ev_mask, s);
+      AHR_QRES_L(DT_BF16, 6, 1);
   } else {
-    if (wide)
-      launch_k<DT_F16, 12>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                           pub, pub_mask, ev_mask, s);
+    if (wide && half)
+      AHR_QRES_L(DT_F16, 12, 2);
+    else if (wide)
+      AHR_QRES_L(DT_F16, 12, 1);
     else
-      launch_k<DT_F16, 6>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags,
-                          pub, pub_mask, ev_mask, s);
+      AHR_QRES_L(DT_F16, 6, 1);
   }
+#undef AHR_QRES_L
 }
 
 }  // namespace qres
