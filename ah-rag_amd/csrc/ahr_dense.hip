@@ -3208,7 +3208,8 @@ bool small_ok(const ahr_index* ix, int B, int k) {
   return small::lds_bytes(ix->row_stride, 16, 1) <= 160 * 1024;
 }
 
-// The k-blocked 256x256 kernel (bf16/f16, k <= 16) from kKB256MinRows corpus rows on: there the
+// The k-blocked 256x256 kernel (bf16/f16, k <= 16) from kKB256MinRows corpus rows on, below the
+// register-resident kernel's batch range (or k in 13..16): there the
 // corpus streams from HBM and its 3-step-deep ring beats the 128x128 kernel's 1-step one (5M
 // rows, B = 1024: 8.11 vs 9.04 ms; 1.25M: 1.97 vs 2.31 ms; 625k: 1.03 vs 1.17 ms; 312k: equal;
 // at 90k, L2/MALL-resident, the 128x128 kernel is ahead, 152 vs 209 us). Debug flags force it
@@ -3234,9 +3235,10 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
   if (ix->debug_flags & kFlagNoQres) return false;
   if (ix->debug_flags & kFlagQres) return true;
   if (ix->debug_flags & kForceFlags) return false;  // another kernel explicitly requested
-  // from kKB256MinRows on the corpus streams from HBM and the k-blocked kernel stays ahead (5M x 768
-  // f16, B = 1024: 7.49 vs 7.71 ms per launch on the same box)
-  return B >= kQresMinBatch && sample_rows_for(ix) > 0 && ix->count >= kQresMinRows && ix->count < kKB256MinRows;
+  // (also past kKB256MinRows, where the corpus streams from HBM: 5M x 768 f16, B = 1024, self-seeded
+  // qres256 6.96 ms vs kb256 7.45 ms per launch on the same box, profiles/r04/ab_sched/c3; round 3's
+  // pre-pass-seeded two-stage form was behind, 7.71 vs 7.49)
+  return B >= kQresMinBatch && sample_rows_for(ix) > 0 && ix->count >= kQresMinRows;
 }
 
 // Self-seeding buffer of the register-resident plan (ahr_qres.hip): the launch tag (advanced on the
@@ -3297,7 +3299,7 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     int want = std::max(1, 256 / p.qblocks);
     want = std::min(want, std::max(1, p.n_row_tiles));
     p.xcd_remap = want >= 8;
-    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : std::max(1, want & ~1);  // even: self-seeding pairs splits
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     return p;
   }
@@ -3627,7 +3629,8 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const int S = sample_rows_for(ix);
   // the register-resident kernel seeds itself (no pre-pass launch) unless kFlagQresPrepass asks for
   // the sampled pre-pass (A/B) or the caller supplies seeds
-  const bool self_seed = p.kernel == KERNEL_QRES && S > 0 && !ix->seed && !(ix->debug_flags & kFlagQresPrepass);
+  const bool self_seed = p.kernel == KERNEL_QRES && S > 0 && !ix->seed && !(ix->debug_flags & kFlagQresPrepass) &&
+                         qres::self_seeds(ix->count, p.n_splits);
   if (ix->seed) {
     thr = ix->seed;  // the caller's valid lower bounds of each query's k-th best score
   } else if (!self_seed && S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {

@@ -114,6 +114,12 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
                                            0, 0);
 }
 
+// with a cache policy: sc1 (16) reads past the CU's L1 (what another CU wrote with sc1 stores)
+__device__ __forceinline__ void blds16_pol(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0,
+                                           16);
+}
+
 // the same with a wave-uniform byte offset added to the global address only, through soffset (an
 // SGPR; the instruction's immediate offset would also shift the LDS destination)
 __device__ __forceinline__ void blds16_soff(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* lds_wave_base) {
@@ -195,6 +201,7 @@ enum : uint32_t {
   kFlagQresPrepass = 1u << 26,   // qres kernel seeded by the sampled pre-pass launch, not by itself (A/B)
   kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first event only, no later rounds (A/B)
   kFlagQresHalfStages = 1u << 28,  // qres at d_pad 768: two 24-KiB stages per block, 3-slot ring (A/B)
+  kFlagQresTrace = 1u << 29,  // qres kernel: per-workgroup timestamps into AHR_QRES_TRACE_PTR (ablation build)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
@@ -207,7 +214,7 @@ constexpr uint32_t kKernelFlags =
 constexpr uint32_t kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
 // every flag ahr_index_set_debug_flags accepts; those that give wrong results need the ablation build
 constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
-                                       kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead;
+                                       kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead | kFlagQresTrace;
 constexpr uint32_t kKnownFlags = kKernelFlags | kWrongResultFlags | kFlagNoTilePrefetch | kFlagNoFold |
                                  kFlagQresPrepass | kFlagQresSeedOnce | kFlagQresHalfStages;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)

@@ -11,7 +11,15 @@ namespace qres {
 
 constexpr int kTQ = 256;     // queries per workgroup: 8 waves x 32
 constexpr int kTR = 32;      // corpus rows per block
-constexpr int kBufCap = 16;  // per-lane survivor buffer (keys) in LDS
+constexpr int kBufCap = 14;  // per-lane survivor buffer (keys) in LDS
+constexpr int kPark = kBufCap - 8;  // self-seeding: block 0's raw scores wait in entries kPark .. kBufCap - 1
+
+// Whether a launch seeds itself: every split has its first two blocks, the splits fit one wave's
+// selection (<= 128) and pair up in the landing zone (even). Otherwise the caller seeds it (the
+// pre-pass) or it runs unseeded.
+__host__ __device__ inline bool self_seeds(int64_t n_rows, int n_splits) {
+  return n_splits >= 2 && n_splits <= 128 && n_splits % 2 == 0 && (n_rows + kTR - 1) / kTR >= 2 * (int64_t)n_splits;
+}
 
 // bf16 / f16 rows of d_pad_bytes = 1536 or 768 (d_pad = 768 or 384), k <= 12: what the kernel is built for.
 bool supported(int dtype, int d_pad_bytes, int k);

@@ -49,6 +49,9 @@ namespace qres {
 // NKT 64-deep k-tiles per row (12 at d_pad 768, 6 at 384), SPB stages per 32-row block: a stage is
 // NKT / SPB k-tiles (24 KiB or a whole 48-KiB block). 24-KiB stages run a 3-slot ring issued two
 // stages ahead; 48-KiB stages a 2-slot ring issued one stage (a whole block) ahead.
+constexpr int kLandBytes = 768;
+static_assert(kPark >= 6, "the replay of a parked block never overtakes its unread quads");
+
 template <int NKT, int SPB>
 struct Cfg {
   static_assert(NKT % (6 * SPB) == 0, "stages of 6 or 12 k-tiles");
@@ -64,10 +67,10 @@ struct Cfg {
   static constexpr int kSS = kSK * 4;             // k16 steps per stage
   // LDS: the ring, the seeding scratch (per wave 1 KiB: what of a seeding event's parked
   // accumulators the free ring slot cannot hold; none with 48-KiB slots), the lane buffers
-  static constexpr int kOffSeed = kSlots * kStage;
-  static constexpr int kSeedBytes = kStage >= 32 * 1024 ? 0 : kWaves * 1024;
-  static constexpr int kOffBuf = kOffSeed + kSeedBytes;
-  static constexpr int kLds = kOffBuf + kBufCap * kThreads * 8;
+  static constexpr int kOffBuf = kSlots * kStage;
+  // the seeding events' landing zone, per wave: 64 published maxima (512 B), 32 seeds (256 B)
+  static constexpr int kOffLand = kOffBuf + kBufCap * kThreads * 8;
+  static constexpr int kLds = kOffLand + kWaves * kLandBytes;
 };
 static_assert(Cfg<12, 2>::kLds <= 160 * 1024 && Cfg<12, 1>::kLds <= 160 * 1024 && Cfg<6, 1>::kLds <= 160 * 1024,
               "LDS budget: one workgroup per CU");
@@ -82,8 +85,8 @@ static_assert(Cfg<12, 2>::kLds <= 160 * 1024 && Cfg<12, 1>::kLds <= 160 * 1024 &
 // 2^m - 2 and an event at the end of block 2^m - 1.
 constexpr uint32_t kSeedWaitTicks = 3000;  // s_memrealtime ticks (100 MHz): a 30-us bound per wait
 __device__ __forceinline__ bool pow2(int x) { return (x & (x - 1)) == 0; }
-__device__ __forceinline__ bool in_sched(uint64_t mask, int bi, int off) {
-  return bi < 64 ? ((mask >> bi) & 1) != 0 : pow2(bi + off);
+__device__ __forceinline__ bool in_sched(uint32_t mask, int bi, int off) {
+  return bi < 32 ? ((mask >> bi) & 1) != 0 : pow2(bi + off);
 }
 
 template <int CTRL, int ROW_MASK>
@@ -149,7 +152,7 @@ template <int DT, int NKT, int SPB, int KCAP, int ABL>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
-    int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t pub_mask, uint64_t ev_mask) {
+    int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t sched) {
   using C = Cfg<NKT, SPB>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -176,12 +179,31 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   const int qw0 = qb * kTQ + wave * 32;
   const bool live = qw0 < n_q;  // wave-uniform: a wave past the batch only stages and syncs
   const int q = qw0 + fr;
-  // self-seeding needs every split's first two blocks and at most 128 splits (grid-uniform)
-  const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && n_blocks >= 2 * n_splits && n_splits <= 128;
+  const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && self_seeds(n_rows, n_splits);
+  // ABL_TRACE (the profiling build only): thread 0 of each workgroup stamps into the buffer passed
+  // as thr_init, 64 u64 per workgroup: [0] s_memrealtime at entry, [1] s_memtime at entry, [2] loop
+  // entry, [3 + j] after stage j's sync (j <= 55), [59] first event entered, [60] selection done,
+  // [61] seed read, [62] s_memrealtime at exit, [63] s_memtime at exit.
+  constexpr bool kTrace = (ABL & ABL_TRACE) != 0;
+  auto stamp = [&](int i, bool core_clock = false) __attribute__((always_inline)) {
+    if constexpr (kTrace) {
+      if (tid == 0)
+        reinterpret_cast<uint64_t*>(const_cast<float*>(thr_init))[(int64_t)blockIdx.x * 64 + i] =
+            core_clock ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(0);
+  stamp(1, true);
 
-  float thr = q < n_q ? (thr_init ? thr_init[q] : -INFINITY) : INFINITY;
+  float thr = q < n_q ? (thr_init && !kTrace ? thr_init[q] : -INFINITY) : INFINITY;
   const uint32_t epoch = pub ? (uint32_t)pub[-1] : 0u;
-  uint64_t* const seeds = pub + (int64_t)qblocks * kTQ * n_splits;
+  // (the seed array's address is recomputed at each use from laundered operands: a live 64-bit
+  // pointer costs two SGPRs the loop does not have)
+  auto seeds_at = [&](int64_t qq) __attribute__((always_inline)) {
+    int qbk = qblocks, ns = n_splits;
+    asm volatile("" : "+s"(qbk), "+s"(ns));
+    return pub + (int64_t)qbk * kTQ * ns + qq;
+  };
 
   // DMA: piece p = wave + 8 i of a stage is k-tile p / 4, rows 8 (p % 4) .. +8; lane l lands at
   // (row 8 (p % 4) + l / 8, physical chunk l % 8) and loads logical chunk (l % 8) ^ swz(row)
@@ -232,8 +254,6 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     asm volatile("" : "+v"(t));
     return lbuf0 + t;
   };
-  // this wave's seeding scratch: a seeding event's parked accumulator tail (1 KiB)
-  unsigned char* const wscr = smem + C::kOffSeed + wave * 1024;
   int nb = 0;
   // keep the k_out best buffered keys; the smallest kept is the lane's k-th best: new threshold
   auto compact = [&]() {
@@ -313,52 +333,85 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     asm volatile("" : "+v"(qq));
     if (!fh && qq < n_q) granule_store(pub + (int64_t)qq * n_splits + split, ((uint64_t)epoch << 32) | ord_f32(pm));
   };
-  // A seeding event: every query j of this wave with j mod n_splits == split, polling (bounded) until
-  // every split's granule of this launch is there (after the first event they all are); the k-th
-  // largest published maximum becomes its seed.
-  auto select_wait = [&]() __attribute__((always_inline)) {
-    const int j0 = wave * 32 + (((split - wave * 32) % n_splits) + n_splits) % n_splits;
-#pragma unroll 1
-    for (int j = j0; j < wave * 32 + 32; j += n_splits) {
-      const int64_t qq = (int64_t)qb * kTQ + j;
-      if (qq >= n_q) break;
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      const uint64_t* src = pub + qq * n_splits;
-      uint32_t v0 = 0, v1 = 0;
-      const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#pragma unroll 1
-      for (;;) {
-        const uint64_t g0 = ln < n_splits ? granule_load(src + ln) : 0;
-        const uint64_t g1 = ln + 64 < n_splits ? granule_load(src + ln + 64) : 0;
-        const bool ok0 = (uint32_t)(g0 >> 32) == epoch, ok1 = (uint32_t)(g1 >> 32) == epoch;
-        v0 = ok0 ? (uint32_t)g0 : 0u;
-        v1 = ok1 ? (uint32_t)g1 : 0u;
-        const int n_ok = __popcll(__ballot(ok0)) + __popcll(__ballot(ok1));
-        if (n_ok >= n_splits || (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > kSeedWaitTicks) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      const uint32_t m = wave_kth(v0, v1, k_out, ln);
-      if (m != 0 && ln == 0) granule_store(seeds + qq, ((uint64_t)epoch << 32) | m);
-    }
-  };
   auto apply_seed = [&](uint64_t g) __attribute__((always_inline)) {  // a seed granule of this launch raises thr
     if (q < n_q && (uint32_t)(g >> 32) == epoch && (uint32_t)g != 0)
       thr = fmaxf(thr, key_score((uint64_t)(uint32_t)g << 32));
   };
-  auto read_wait = [&]() __attribute__((always_inline)) {  // poll (bounded) until this launch's seeds are there
-    uint64_t g = 0;
-    int qq = q;
-    asm volatile("" : "+v"(qq));
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  // Seeding events. Granule and seed reads go through the wave's LDS landing zone by buffer
+  // LDS-DMA (sc1), so no register is held between two events: a later event consumes what the
+  // previous one's loads landed (a landing not complete yet only leaves an earlier round's — still
+  // valid — or zeroed granules) and issues the next, never waiting; the first polls (bounded) until
+  // every split's block-0 granule, then every seed, of this launch is there. Granules: lane l < 32
+  // of a selecting wave loads maxima 2p, 2p + 1 of its selected query i = l / np (p = l % np,
+  // np = n_splits / 2; past 64 splits only the first 64: a subset, a weaker still valid bound);
+  // seeds: lane l < 16 loads the seeds of the wave's queries 2l, 2l + 1. One code site serves
+  // every event (two would not fit the register budget).
+  unsigned char* const land = smem + C::kOffLand + wave * kLandBytes;
+  if (tid % 64 < kLandBytes / 16) *reinterpret_cast<u32x4*>(land + lane * 16) = u32x4{0, 0, 0, 0};
+  auto event_site = [&](bool first) __attribute__((always_inline)) {
+    int sp = split, ns = n_splits;
+    asm volatile("" : "+s"(sp), "+s"(ns));
+    const int np = ns >= 128 ? 32 : ns / 2;  // lanes per selected query
+    const int j0 = wave * 32 + (((sp - wave * 32) % ns) + ns) % ns;
+    const int cnt = (ns & 1) || j0 >= wave * 32 + 32 ? 0 : (wave * 32 + 31 - j0) / ns + 1;  // wave-uniform
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int my_i = ln / np;
+    const int64_t my_q = (int64_t)qb * kTQ + j0 + my_i * ns;
+    const bool sel_lane = ln < 32 && my_i < cnt && my_q < n_q;
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(pub, (uint32_t)((int64_t)qblocks * kTQ * (ns + 1) * 8));
+    auto issue_granules = [&]() __attribute__((always_inline)) {
+      if (sel_lane) blds16_pol(r, (uint32_t)((my_q * ns + 2 * (ln - my_i * np)) * 8), land);
+    };
+    auto issue_seeds = [&]() __attribute__((always_inline)) {
+      if (ln < 16) blds16_pol(r, (uint32_t)(((int64_t)qblocks * kTQ * ns + (int64_t)qb * kTQ + wave * 32 + 2 * ln) * 8),
+                              land + 512);
+    };
+    auto landed = [&](bool seeds_part) __attribute__((always_inline)) {  // bounded poll (first event)
+      const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
-    for (;;) {
-      g = qq < n_q ? granule_load(seeds + qq) : 0;
-      const bool ok = qq >= n_q || (uint32_t)(g >> 32) == epoch;
-      if (__ballot(!ok) == 0 || (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > kSeedWaitTicks) break;
-      __builtin_amdgcn_s_sleep(2);
+      for (;;) {
+        if (seeds_part)
+          issue_seeds();
+        else
+          issue_granules();
+        wait_vm<0>();
+        asm volatile("" ::: "memory");
+        bool ok;
+        if (seeds_part) {
+          ok = q >= n_q || *reinterpret_cast<const uint32_t*>(land + 512 + fr * 8 + 4) == epoch;
+        } else {
+          const u32x4 g = *reinterpret_cast<const u32x4*>(land + ln * 16);
+          ok = !sel_lane || (g[1] == epoch && g[3] == epoch);
+        }
+        if (__ballot(!ok) == 0 || (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > kSeedWaitTicks) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    };
+    if (first) {
+      stamp(59);
+      landed(false);
     }
-    apply_seed(g);
+    if (cnt > 0) {  // the k-th largest of each selected query's published maxima
+      const u32x4 g = *reinterpret_cast<const u32x4*>(land + ln * 16);
+      const uint32_t v0 = sel_lane && g[1] == epoch ? g[0] : 0u;
+      const uint32_t v1 = sel_lane && g[3] == epoch ? g[2] : 0u;
+#pragma unroll 1
+      for (int i = 0; i < cnt; ++i) {
+        const int64_t qq = (int64_t)qb * kTQ + j0 + i * ns;
+        if (qq >= n_q) break;
+        const uint32_t m = wave_kth(my_i == i ? v0 : 0u, my_i == i ? v1 : 0u, k_out, ln);
+        if (m != 0 && ln == 0) granule_store(seeds_at(qq), ((uint64_t)epoch << 32) | m);
+      }
+    }
+    if (first) {
+      stamp(60);
+      landed(true);
+      stamp(61);
+    }
+    apply_seed(*reinterpret_cast<const uint64_t*>(land + 512 + fr * 8));
+    issue_granules();  // for the next event
+    issue_seeds();
   };
   // block 0's raw scores parked in the upper half of the lane buffer (entries 8 .. 15, two floats
   // each) until the first seed; replayed quad by quad from the bottom while the appends fill the
@@ -368,7 +421,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     uint64_t* const lbuf = lb();
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      lbuf[(8 + e) * kThreads] = ((uint64_t)__float_as_uint(acc[2 * e + 1]) << 32) | __float_as_uint(acc[2 * e]);
+      lbuf[(kPark + e) * kThreads] = ((uint64_t)__float_as_uint(acc[2 * e + 1]) << 32) | __float_as_uint(acc[2 * e]);
   };
   auto replay = [&](int r0) __attribute__((always_inline)) {
     asm volatile("" : "+s"(r0));  // (not loop-invariant to LLVM: it would hoist all 16 row keys and spill them)
@@ -376,7 +429,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     uint64_t* const lbuf = lb();
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) {
-      const uint64_t a = lbuf[(8 + 2 * qd) * kThreads], b = lbuf[(9 + 2 * qd) * kThreads];
+      const uint64_t a = lbuf[(kPark + 2 * qd) * kThreads], b = lbuf[(kPark + 1 + 2 * qd) * kThreads];
       const float v0 = __uint_as_float((uint32_t)a), v1 = __uint_as_float((uint32_t)(a >> 32));
       const float v2 = __uint_as_float((uint32_t)b), v3 = __uint_as_float((uint32_t)(b >> 32));
       if (fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)) >= thr) screen_quad(v0, v1, v2, v3, r0 + 8 * qd + 4 * fh, ragged);
@@ -448,45 +501,16 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       return;
     }
     screen_quads(acc, r0);
-    if (ss && in_sched(pub_mask, bi, 2)) publish();
+    if (ss && in_sched((uint32_t)sched, bi, 2)) publish();
   };
-  // A seeding event at the end of a block, before its screening: the block's 16 accumulators wait
-  // in LDS (in the ring slot that is free then — stage j - 1's, whose refill is issued only after
-  // this path — and, for 24-KiB slots, 4 of them in the wave's scratch), so the waits (and, at the
-  // first event, the replay of block 0) hold no accumulator registers; the main loop has none to
-  // spare.
-  auto seed_event = [&](int j, bool first) __attribute__((always_inline)) {
-    float* const pa = reinterpret_cast<float*>(slot_of(j - 1)) + tid * 4;
-    float* const pb = reinterpret_cast<float*>(wscr) + lane * 4;
-    constexpr int kInSlot = C::kStage / (kThreads * 16) * 4;  // floats per lane the slot holds
-    auto at = [&](int i) __attribute__((always_inline)) { return i < kInSlot ? pa + (i >> 2) * kThreads * 4 : pb; };
-#pragma unroll
-    for (int i = 0; i < 16; i += 4) *reinterpret_cast<f32x4*>(at(i)) = f32x4{acc[i], acc[i + 1], acc[i + 2], acc[i + 3]};
-    asm volatile("" ::: "memory");
-    select_wait();
-    read_wait();
-    if (first) replay(b_begin * kTR);
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < 16; i += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(at(i));
-      acc[i] = v[0];
-      acc[i + 1] = v[1];
-      acc[i + 2] = v[2];
-      acc[i + 3] = v[3];
-    }
-  };
+  stamp(2);
 #pragma unroll 1
   for (int j = 0; j <= n_st; ++j) {
     stage_sync(j);
+    if (j <= 55) stamp(3 + j);
     const bool bend = j >= C::kSPB && j % C::kSPB == 0;  // block j / kSPB - 1 ended with stage j - 1
     const int bi = j / C::kSPB - 1;
     const bool first = ss && j == 2 * C::kSPB;  // uniform
-    const bool event = first || (ss && bend && in_sched(ev_mask, bi, 1));
-    if (event) {
-      if (live) seed_event(j, first);
-      lds_barrier();  // every wave's parked accumulators are back before the slot is refilled
-    }
     if (j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + C::kAhead);
     if (!live) continue;
     const bool mma = j < n_st;
@@ -494,7 +518,14 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       fa[0] = frag(j, 0);
       fa[1] = frag(j, 1);
     }
-    if (bend) finish_block(bi);
+    // block bi's screening, then a seeding event (the first one before block 1's screening, which
+    // then runs with the first seed after block 0's parked scores)
+    if (bend && !first) finish_block(bi);
+    if (ss && bend && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
+    if (first) {
+      replay(b_begin * kTR);
+      finish_block(bi);
+    }
     if (mma) {
       if (C::kSPB == 1 || !(j & 1))
         stage_mma(std::integral_constant<int, 0>{}, j);
@@ -530,6 +561,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     for (int j = 0; j < KCAP; ++j)
       if (j < k_out) dst[j] = L[j];
   }
+  stamp(62);
+  stamp(63, true);
 }
 
 bool supported(int dtype, int d_pad_bytes, int k) {
@@ -552,11 +585,17 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
   if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
     const int abl = ((flags & kFlagSkipEpilogue) ? ABL_NOSCREEN : 0) | ((flags & kFlagNoLoads) ? ABL_NOLOADS : 0) |
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
-                    ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0);
+                    ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0) | ((flags & kFlagQresTrace) ? ABL_TRACE : 0);
+    if (abl & ABL_TRACE) {  // the stamps go to the buffer AHR_QRES_TRACE_PTR names (device address)
+      const char* e = getenv("AHR_QRES_TRACE_PTR");
+      if (!e) return;
+      thr = reinterpret_cast<const float*>((uintptr_t)strtoull(e, nullptr, 16));
+    }
 #define AHR_QRES_ABL(V) \
   case V: launch_t<DT, NKT, SPB, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
+      AHR_QRES_ABL(32)
       default: break;
     }
 #undef AHR_QRES_ABL
@@ -566,8 +605,8 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
   constexpr int lds = Cfg<NKT, SPB>::kLds;
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), lds, s, rows, qfrag,
-                     row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask,
-                     ev_mask);
+                     row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub,
+                     (pub_mask & 0xffffffffull) | (ev_mask << 32));
 }
 
 template <int DT, int NKT, int SPB>

@@ -26,7 +26,7 @@ __device__ __forceinline__ void wait_vm() {
 // screening, 2 = no corpus DMA after the first stages, 4 = no DMA waits, 8 = no stage barriers,
 // 16 = no LDS fragment reads (a register stands in). Compile-time, so the production code path is
 // the ABL = 0 instantiation untouched. Every nonzero combination gives wrong results.
-enum { ABL_NOSCREEN = 1, ABL_NOLOADS = 2, ABL_NOWAIT = 4, ABL_NOBARRIER = 8, ABL_NOREAD = 16 };
+enum { ABL_NOSCREEN = 1, ABL_NOLOADS = 2, ABL_NOWAIT = 4, ABL_NOBARRIER = 8, ABL_NOREAD = 16, ABL_TRACE = 32 };
 
 }  // namespace qres
 }  // namespace dense

@@ -16,7 +16,7 @@ sys.path[:0] = [os.path.join(ROOT, "ah-rag_amd"), ROOT]
 import torch  # noqa: E402
 
 from ah_rag.embeddings import DenseIndex  # noqa: E402
-from ah_rag.synthetic import HOTPOT_90K, SYNTH_5M, SyntheticCorpus  # noqa: E402
+from ah_rag.synthetic import HOTPOT_90K, SYNTH_5M, CorpusSpec, SyntheticCorpus  # noqa: E402
 
 
 def run(ix, q, k, steps):
@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--variants", default="prod:-1:0,tile128:-1:8,kb256:-1:131072,no_prepass:0:0,gemm_only:-1:2,max_only:-1:256")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    spec = HOTPOT_90K if a.workload == "hotpot90k" else SYNTH_5M
+    spec = {"hotpot90k": HOTPOT_90K, "hotpot90k_d384": CorpusSpec(dim=384), "synth5m": SYNTH_5M}[a.workload]
     c = SyntheticCorpus(spec, dev)
     rows = c.rows()
     if a.rows:
