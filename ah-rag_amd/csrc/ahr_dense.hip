@@ -3243,7 +3243,8 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
 
 // Self-seeding buffer of the register-resident plan (ahr_qres.hip): the launch tag (advanced on the
 // device by each query conversion), then per query slot of the padded batch one published maximum
-// per split (at most kQresMaxSplits), then one seed. Zeroed when allocated (tag 0 is never a
+// per split (at most kQresMaxSplits), then one seed (and, past the seeds, the spare slots a
+// selection with no seed writes to; the kernel uses at most 128 splits, so they fit). Zeroed when allocated (tag 0 is never a
 // launch's), so a granule is only ever this workspace's own.
 constexpr int64_t kQresMaxSplits = 256;
 int ensure_ss(ahr_index* ix, hipStream_t s) {
@@ -3260,17 +3261,17 @@ int ensure_ss(ahr_index* ix, hipStream_t s) {
 }
 
 // The register-resident kernel's self-seeding schedule over a split's block index: publications
-// after blocks 0, 2, 6, 14, 30 and seeding events at the ends of blocks 1 (the first, waiting), 3,
-// 7, 15, 31 — each event's selection uses the maxima of the publication one block before it, so
-// the seed tightens from a 2-block-per-split sample to a 31-block one as the splits advance.
+// after blocks 0, 2, 4, 6 and then every 4th to 30, seeding events at the ends of blocks 1 (the
+// first, waiting), 3, 5, 7 and every 4th to 31 (then every 8 blocks: ahr_qres.hip). A later event
+// selects from the granules the previous one read and applies the seeds it read, so a seed lags its
+// publication by two events; dense early events make up for that while the threshold is loose.
 // AHR_QRES_PUB / AHR_QRES_EV (hex bit masks) override it for tuning.
 struct QresSchedule {
   uint64_t pub, ev;
 };
 inline QresSchedule qres_schedule() {
   static const QresSchedule sch = [] {
-    QresSchedule d{(1ull << 0) | (1ull << 2) | (1ull << 6) | (1ull << 14) | (1ull << 30),
-                   (1ull << 3) | (1ull << 7) | (1ull << 15) | (1ull << 31)};
+    QresSchedule d{0x44444455ull, 0x888888a8ull};
     if (const char* e = getenv("AHR_QRES_PUB")) d.pub = strtoull(e, nullptr, 16);
     if (const char* e = getenv("AHR_QRES_EV")) d.ev = strtoull(e, nullptr, 16);
     return d;

@@ -200,8 +200,9 @@ enum : uint32_t {
   kFlagNoLdsRead = 1u << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
   kFlagQresPrepass = 1u << 26,   // qres kernel seeded by the sampled pre-pass launch, not by itself (A/B)
   kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first event only, no later rounds (A/B)
-  kFlagQresHalfStages = 1u << 28,  // qres at d_pad 768: two 24-KiB stages per block, 3-slot ring (A/B)
   kFlagQresTrace = 1u << 29,  // qres kernel: per-workgroup timestamps into AHR_QRES_TRACE_PTR (ablation build)
+  kFlagQresEvNoSel = 1u << 30,   // qres seeding events without the selection (wrong seeds: ablation build)
+  kFlagQresEvNoIssue = 1u << 31, // qres seeding events without the landing reads (ablation build)
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in
@@ -214,9 +215,10 @@ constexpr uint32_t kKernelFlags =
 constexpr uint32_t kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
 // every flag ahr_index_set_debug_flags accepts; those that give wrong results need the ablation build
 constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
-                                       kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead | kFlagQresTrace;
+                                       kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead | kFlagQresTrace |
+                                       kFlagQresEvNoSel | kFlagQresEvNoIssue;
 constexpr uint32_t kKnownFlags = kKernelFlags | kWrongResultFlags | kFlagNoTilePrefetch | kFlagNoFold |
-                                 kFlagQresPrepass | kFlagQresSeedOnce | kFlagQresHalfStages;
+                                 kFlagQresPrepass | kFlagQresSeedOnce;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 }  // namespace dense

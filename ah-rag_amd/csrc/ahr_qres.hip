@@ -12,16 +12,16 @@
 // from LDS) against its own queries with one v_mfma_f32_32x32x16 chain per block, so a corpus
 // byte brought in is used by 8 waves.
 //
-// * Corpus: 32-row blocks in stages of 6 k-tiles (64-deep, 128 B per row: 24 KiB; 2 stages per
-//   block at d_pad = 768, 1 at 384); a 4-slot ring filled by buffer LDS-DMA two stages ahead
-//   (1-KiB pieces of 8 whole 128-B rows, 3 per wave per stage), the XOR chunk swizzle of the tile
-//   kernels (conflict-free ds_read_b128). One barrier per stage.
+// * Corpus: 32-row blocks. At d_pad = 768 one 48-KiB stage per block in a 2-slot ring issued a
+//   whole block ahead (two 24-KiB stages per block in a 3-slot ring measured 9 us slower at C2); at
+//   384 one 24-KiB stage per block in a 3-slot ring issued two blocks ahead. Buffer LDS-DMA of 1-KiB pieces (8 whole 128-B rows), the XOR chunk swizzle of
+//   the tile kernels (conflict-free ds_read_b128). One barrier per stage.
 // * Scores: the k-order, fragment map and accumulation chain of topk_tilelane_kernel (step s of
 //   a row covers k = [16 s, 16 s + 16), lane half fh holding 8 of them; the chain starts from 0),
 //   so every score is bitwise the tile kernel's.
 // * Top-k: a lane holds one query column x 16 rows of each block. Its 16 scores are screened
 //   against the lane's threshold: the block max in the common case, and for the rare passing
-//   scores one 8-B append to the lane's 16-entry LDS buffer. A full buffer is compacted in place
+//   scores one 8-B append to the lane's 14-entry LDS buffer. A full buffer is compacted in place
 //   to its k best, which raises the threshold. At the end each lane sorts its buffer into a
 //   register list (the query registers are dead by then) and the two lanes of a query merge:
 //   one list per (query, split).
@@ -33,13 +33,15 @@
 //   the k-th best — and publishes it as the query's seed, which every split reads. First round:
 //   maxima of each split's first block (a 2,048-row sample at C2), the block's raw scores parked
 //   in the lane buffer meanwhile and screened against the seed once it is there (a short bounded
-//   wait at the end of block 1); later rounds (maxima over 4, 8, 16, ... blocks) tighten it
-//   without waiting. Granules carry the launch's epoch, so a stale or absent one only weakens
-//   the seed, never invalidates it; every wait is bounded, so nothing assumes co-residency.
+//   wait at the end of block 1); later rounds (maxima over 3, 7, 15, ... blocks) tighten it and
+//   never wait: their reads land in a per-wave LDS zone by buffer LDS-DMA and are consumed by the
+//   next round. Granules carry the launch's epoch, so a stale or absent one only weakens the seed,
+//   never invalidates it; every wait is bounded, so nothing assumes co-residency.
 // * Query fragments come from a fragment-major copy of the converted queries (launch_frag):
 //   one coalesced 1-KiB load per wave per k16 step.
 // * Budget: NKT*16 query VGPRs + 16 accumulators + fragments in flight <= 256 (two waves per SIMD,
-//   one workgroup of 8 waves per CU); LDS 96 KiB ring + 64 KiB lane buffers = 160 KiB.
+//   one workgroup of 8 waves per CU); LDS at d_pad 768: 96 KiB ring + 56 KiB lane buffers + 6 KiB
+//   landing zones = 158 KiB.
 #include "ahr_qres_common.h"
 
 namespace ahr {
@@ -70,23 +72,24 @@ struct Cfg {
   static constexpr int kOffBuf = kSlots * kStage;
   // the seeding events' landing zone, per wave: 64 published maxima (512 B), 32 seeds (256 B)
   static constexpr int kOffLand = kOffBuf + kBufCap * kThreads * 8;
-  static constexpr int kLds = kOffLand + kWaves * kLandBytes;
+  // the seeding events' per-lane table (see event_site): 4 B per lane
+  static constexpr int kOffTab = kOffLand + kWaves * kLandBytes;
+  static constexpr int kLds = kOffTab + kThreads * 4;
 };
-static_assert(Cfg<12, 2>::kLds <= 160 * 1024 && Cfg<12, 1>::kLds <= 160 * 1024 && Cfg<6, 1>::kLds <= 160 * 1024,
+static_assert(Cfg<12, 1>::kLds <= 160 * 1024 && Cfg<6, 1>::kLds <= 160 * 1024,
               "LDS budget: one workgroup per CU");
 
-// Self-seeding schedule (uniform, over a split's block index bi < 64; the host passes it): after
-// block bi with bit bi of pub_mask set, a split publishes its running per-query maxima; at the end
-// of block bi with bit bi of ev_mask set, a seeding event: the selecting splits take the k-th
-// largest published maxima as seeds, every split reads its queries' seeds. The first event (block
-// 1, after the block-0 publication) waits, bounded, for every granule and seed; later events use
-// what is there (an earlier round's granule is still a valid lower bound), so they never wait.
-// From block 64 on (large corpora) the schedule continues geometrically: a publication after block
-// 2^m - 2 and an event at the end of block 2^m - 1.
+// Self-seeding schedule (uniform, over a split's block index; the host passes it, publications in
+// the low 32 bits, events in the high): after block bi < 32 with its publication bit set, a split
+// publishes its running per-query maxima; at the end of block bi with its event bit set, a seeding
+// event: the selecting splits take the k-th largest published maxima (landed since the previous
+// event) as seeds, every split applies the seeds that landed, and both reads are issued again. The
+// first event (block 1, after the block-0 publication) waits, bounded, for every granule and seed.
+// From block 32 on (large corpora) the schedule continues every 8 blocks: a publication after block
+// 8m - 2 and an event at the end of block 8m - 1.
 constexpr uint32_t kSeedWaitTicks = 3000;  // s_memrealtime ticks (100 MHz): a 30-us bound per wait
-__device__ __forceinline__ bool pow2(int x) { return (x & (x - 1)) == 0; }
 __device__ __forceinline__ bool in_sched(uint32_t mask, int bi, int off) {
-  return bi < 32 ? ((mask >> bi) & 1) != 0 : pow2(bi + off);
+  return bi < 32 ? ((mask >> bi) & 1) != 0 : (bi + off) % 8 == 0;
 }
 
 template <int CTRL, int ROW_MASK>
@@ -122,6 +125,21 @@ __device__ __forceinline__ uint32_t wave_kth(uint32_t v0, uint32_t v1, int k, in
     }
   }
   return m;
+}
+
+// An admissible k-th largest of the wave's nonzero values (lane l holds v0, v1): the largest t on a
+// grid of 2^12 with at least k values >= t. Never above the exact k-th largest, so still a valid
+// lower bound (ord space: at most 2^-11 of the score below it); 0 if fewer than k are nonzero. 20
+// ballot rounds, scalar between them: ~4x fewer instructions than k rounds of wave_kth.
+__device__ __forceinline__ uint32_t wave_kth_grid(uint32_t v0, uint32_t v1, int k) {
+  uint32_t t = 0;
+#pragma unroll
+  for (int b = 31; b >= 12; --b) {
+    const uint32_t c = t | (1u << b);
+    const int n = __popcll(__ballot(v0 >= c)) + __popcll(__ballot(v1 >= c));
+    t = n >= k ? c : t;
+  }
+  return t;
 }
 
 __device__ __forceinline__ uint64_t granule_load(const uint64_t* p) {
@@ -327,11 +345,18 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // (the seeding paths launder the lane's query index through an empty asm: otherwise LLVM hoists
   // their 64-bit granule addresses out of the main loop, and the extra registers spill the
   // resident fragments)
+  // Vector-memory operations this wave issued after its ring pieces in the current iteration (the
+  // publication store, the event's seed stores and landing loads), counted exactly: the next stage
+  // sync waits for all but these (vmcnt counts in issue order), so a write-through store or a
+  // cross-XCD read never holds up the ring. Each counted site issues exactly one instruction per
+  // wave (some lane is always active there).
+  int young = 0;
   auto publish = [&]() __attribute__((always_inline)) {
     const float pm = fmaxf(rm, __shfl_xor(rm, 32, 64));  // the query's max over this split's rows
     int qq = q;
     asm volatile("" : "+v"(qq));
     if (!fh && qq < n_q) granule_store(pub + (int64_t)qq * n_splits + split, ((uint64_t)epoch << 32) | ord_f32(pm));
+    ++young;
   };
   auto apply_seed = [&](uint64_t g) __attribute__((always_inline)) {  // a seed granule of this launch raises thr
     if (q < n_q && (uint32_t)(g >> 32) == epoch && (uint32_t)g != 0)
@@ -348,24 +373,56 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // every event (two would not fit the register budget).
   unsigned char* const land = smem + C::kOffLand + wave * kLandBytes;
   if (tid % 64 < kLandBytes / 16) *reinterpret_cast<u32x4*>(land + lane * 16) = u32x4{0, 0, 0, 0};
-  auto event_site = [&](bool first) __attribute__((always_inline)) {
-    int sp = split, ns = n_splits;
-    asm volatile("" : "+s"(sp), "+s"(ns));
+  // The split selects for the queries j = split + m n_splits of its query block; the m-th goes to
+  // wave m % 8, so the selecting waves spread over the four SIMDs (waves w and w + 4 share one):
+  // a selection then runs beside the other wave's MFMA chain instead of stalling both.
+  // Per-lane table, built once (the divisions stay out of the loop): lane l < 32 of a wave, its
+  // granule read (bit 31: a selecting lane; bits 24..29: its query i, the wave's i-th; bits 0..23:
+  // the byte offset in the self-seeding buffer); lanes 48..52 the wave's count of selected queries,
+  // the first one's index in the query block, the buffer's byte size, the offset of the wave's
+  // seeds and the index step between its selected queries.
+  uint32_t* const tab = reinterpret_cast<uint32_t*>(smem + C::kOffTab) + wave * 64;
+  if (ss) {
+    const int ns = n_splits;
     const int np = ns >= 128 ? 32 : ns / 2;  // lanes per selected query
-    const int j0 = wave * 32 + (((sp - wave * 32) % ns) + ns) % ns;
-    const int cnt = (ns & 1) || j0 >= wave * 32 + 32 ? 0 : (wave * 32 + 31 - j0) / ns + 1;  // wave-uniform
+    const int j0 = split + wave * ns;
+    int cnt = 0;
+    for (int j = j0; j < kTQ && (int64_t)qb * kTQ + j < n_q; j += kWaves * ns) ++cnt;
+    uint32_t e = 0;
+    if (lane < 32) {
+      const int i = lane / np;
+      const int64_t qq = (int64_t)qb * kTQ + j0 + i * kWaves * ns;
+      e = i < cnt ? 0x80000000u | ((uint32_t)i << 24) | (uint32_t)((qq * ns + 2 * (lane - i * np)) * 8) : 0u;
+    } else if (lane == 48) {
+      e = (uint32_t)cnt;
+    } else if (lane == 49) {
+      e = (uint32_t)j0;
+    } else if (lane == 52) {
+      e = (uint32_t)(kWaves * ns);
+    } else if (lane == 50) {
+      e = (uint32_t)((int64_t)qblocks * kTQ * (ns + 1) * 8);
+    } else if (lane == 51) {
+      e = (uint32_t)(((int64_t)qblocks * kTQ * ns + (int64_t)qb * kTQ + wave * 32) * 8);
+    }
+    tab[lane] = e;
+  }
+  auto event_site = [&](bool first) __attribute__((always_inline)) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int my_i = ln / np;
-    const int64_t my_q = (int64_t)qb * kTQ + j0 + my_i * ns;
-    const bool sel_lane = ln < 32 && my_i < cnt && my_q < n_q;
-    const __amdgpu_buffer_rsrc_t r = tile_rsrc(pub, (uint32_t)((int64_t)qblocks * kTQ * (ns + 1) * 8));
-    auto issue_granules = [&]() __attribute__((always_inline)) {
-      if (sel_lane) blds16_pol(r, (uint32_t)((my_q * ns + 2 * (ln - my_i * np)) * 8), land);
+    const uint32_t e = tab[ln];
+    const u32x4 uni = *reinterpret_cast<const u32x4*>(tab + 48);
+    const int jstep = __builtin_amdgcn_readfirstlane((int)tab[52]);
+    const int cnt = __builtin_amdgcn_readfirstlane((int)uni[0]);
+    const int j0 = __builtin_amdgcn_readfirstlane((int)uni[1]);
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(pub, (uint32_t)__builtin_amdgcn_readfirstlane((int)uni[2]));
+    const uint32_t seed_off = (uint32_t)__builtin_amdgcn_readfirstlane((int)uni[3]);
+    const bool sel_lane = (e >> 31) != 0;
+    const int my_i = (int)((e >> 24) & 63);
+    auto issue_granules = [&]() __attribute__((always_inline)) {  // lanes past the selection read zeros (out of range)
+      if (ln < 32) blds16_pol(r, sel_lane ? (e & 0xffffffu) : 0x7ffffff0u, land);
     };
     auto issue_seeds = [&]() __attribute__((always_inline)) {
-      if (ln < 16) blds16_pol(r, (uint32_t)(((int64_t)qblocks * kTQ * ns + (int64_t)qb * kTQ + wave * 32 + 2 * ln) * 8),
-                              land + 512);
+      if (ln < 16) blds16_pol(r, seed_off + 16 * ln, land + 512);
     };
     auto landed = [&](bool seeds_part) __attribute__((always_inline)) {  // bounded poll (first event)
       const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -391,27 +448,33 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (first) {
       stamp(59);
       landed(false);
+      young = 0;  // everything this wave issued so far has completed
     }
-    if (cnt > 0) {  // the k-th largest of each selected query's published maxima
+    if (!(ABL & ABL_EV_NOSEL) && cnt > 0) {  // the k-th largest of each selected query's published maxima
       const u32x4 g = *reinterpret_cast<const u32x4*>(land + ln * 16);
       const uint32_t v0 = sel_lane && g[1] == epoch ? g[0] : 0u;
       const uint32_t v1 = sel_lane && g[3] == epoch ? g[2] : 0u;
 #pragma unroll 1
       for (int i = 0; i < cnt; ++i) {
-        const int64_t qq = (int64_t)qb * kTQ + j0 + i * ns;
-        if (qq >= n_q) break;
-        const uint32_t m = wave_kth(my_i == i ? v0 : 0u, my_i == i ? v1 : 0u, k_out, ln);
-        if (m != 0 && ln == 0) granule_store(seeds_at(qq), ((uint64_t)epoch << 32) | m);
+        const int64_t qq = (int64_t)qb * kTQ + j0 + i * jstep;
+        const uint32_t m = wave_kth_grid(my_i == i ? v0 : 0u, my_i == i ? v1 : 0u, k_out);
+        // (no seed: the store goes to the spare slot past the seeds, keeping the count exact)
+        if (ln == 0) granule_store(seeds_at(qq) + (m != 0 ? 0 : (int64_t)qblocks * kTQ), ((uint64_t)epoch << 32) | m);
+        ++young;
       }
     }
     if (first) {
       stamp(60);
       landed(true);
       stamp(61);
+      young = 0;
     }
     apply_seed(*reinterpret_cast<const uint64_t*>(land + 512 + fr * 8));
-    issue_granules();  // for the next event
-    issue_seeds();
+    if constexpr (!(ABL & ABL_EV_NOISSUE)) {
+      issue_granules();  // for the next event
+      issue_seeds();
+      young += 2;
+    }
   };
   // block 0's raw scores parked in the upper half of the lane buffer (entries 8 .. 15, two floats
   // each) until the first seed; replayed quad by quad from the bottom while the appends fill the
@@ -439,13 +502,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // Sync j: this wave's pieces of stage j landed (with a 3-slot ring stage j + 1 may stay in
   // flight), then the barrier: everyone's stage j landed, and everyone is done with stage j - 1,
   // whose slot takes stage j + kAhead.
-  auto stage_sync = [&](int j) __attribute__((always_inline)) {
-    if (!(ABL & ABL_NOWAIT)) {
-      if (C::kAhead == 2 && j + 1 < n_st)
-        wait_vm<C::kPPW>();
-      else
-        wait_vm<0>();
-    }
+  auto stage_sync = [&](int j, int y) __attribute__((always_inline)) {
+    if (!(ABL & ABL_NOWAIT)) wait_vm_dyn((C::kAhead == 2 && j + 1 < n_st ? C::kPPW : 0) + __builtin_amdgcn_readfirstlane(y));
     if (!(ABL & ABL_NOBARRIER)) lds_barrier();
   };
   // A fragment of k16 step s of stage st: k-tile s / 4, logical chunk 2 (s % 4) + fh of row fr,
@@ -506,7 +564,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   stamp(2);
 #pragma unroll 1
   for (int j = 0; j <= n_st; ++j) {
-    stage_sync(j);
+    stage_sync(j, young);
+    young = 0;
     if (j <= 55) stamp(3 + j);
     const bool bend = j >= C::kSPB && j % C::kSPB == 0;  // block j / kSPB - 1 ended with stage j - 1
     const int bi = j / C::kSPB - 1;
@@ -585,7 +644,8 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
   if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
     const int abl = ((flags & kFlagSkipEpilogue) ? ABL_NOSCREEN : 0) | ((flags & kFlagNoLoads) ? ABL_NOLOADS : 0) |
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
-                    ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0) | ((flags & kFlagQresTrace) ? ABL_TRACE : 0);
+                    ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0) | ((flags & kFlagQresTrace) ? ABL_TRACE : 0) |
+                    ((flags & kFlagQresEvNoSel) ? ABL_EV_NOSEL : 0) | ((flags & kFlagQresEvNoIssue) ? ABL_EV_NOISSUE : 0);
     if (abl & ABL_TRACE) {  // the stamps go to the buffer AHR_QRES_TRACE_PTR names (device address)
       const char* e = getenv("AHR_QRES_TRACE_PTR");
       if (!e) return;
@@ -595,7 +655,7 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
   case V: launch_t<DT, NKT, SPB, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
-      AHR_QRES_ABL(32)
+      AHR_QRES_ABL(32) AHR_QRES_ABL(64) AHR_QRES_ABL(128) AHR_QRES_ABL(192)
       default: break;
     }
 #undef AHR_QRES_ABL
@@ -625,25 +685,20 @@ void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t
             int n_rows, int B, uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks,
             int flags, uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
   const bool wide = d_pad_bytes == 12 * kRowBytes;
-  const bool half = (flags & kFlagQresHalfStages) != 0;  // d_pad 768: two 24-KiB stages per block
   pub_mask |= 1;  // block 0's maxima: the first event's sample
-#define AHR_QRES_L(D, N, S) \
-  launch_k<D, N, S>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags, pub, \
+#define AHR_QRES_L(D, N) \
+  launch_k<D, N, 1>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags, pub, \
                     pub_mask, ev_mask, s)
   if (dtype == AHR_BF16) {
-    if (wide && half)
-      AHR_QRES_L(DT_BF16, 12, 2);
-    else if (wide)
-      AHR_QRES_L(DT_BF16, 12, 1);
+    if (wide)
+      AHR_QRES_L(DT_BF16, 12);
     else
-      AHR_QRES_L(DT_BF16, 6, 1);
+      AHR_QRES_L(DT_BF16, 6);
   } else {
-    if (wide && half)
-      AHR_QRES_L(DT_F16, 12, 2);
-    else if (wide)
-      AHR_QRES_L(DT_F16, 12, 1);
+    if (wide)
+      AHR_QRES_L(DT_F16, 12);
     else
-      AHR_QRES_L(DT_F16, 6, 1);
+      AHR_QRES_L(DT_F16, 6);
   }
 #undef AHR_QRES_L
 }
