@@ -3116,6 +3116,12 @@ struct ahr_index {
   // call's stream (ahr_index_profile_begin / _end).
   std::vector<hipEvent_t> prof_events;
   int prof_max_calls = 0;
+  // The register-resident kernel fills every CU and its first seeding event waits (bounded) for
+  // every split: a batch of this plan on one workspace's stream starts after the previous one's
+  // merge on another (its completion event), so no workgroup of another batch delays its start.
+  // (Two batches in flight then gain nothing over one: bench.py runs this plan with one.)
+  hipEvent_t qres_done = nullptr;
+  hipStream_t qres_stream = nullptr;
   int prof_calls = 0;
   uint32_t* fold_ctr() const { return reinterpret_cast<uint32_t*>(part + part_cap); }
 };
@@ -3248,6 +3254,7 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
 // launch's), so a granule is only ever this workspace's own.
 constexpr int64_t kQresMaxSplits = 256;
 int ensure_ss(ahr_index* ix, hipStream_t s) {
+  if (!ix->qres_done) AHR_HIP(hipEventCreateWithFlags(&ix->qres_done, hipEventDisableTiming));
   const int64_t need = 1 + ix->q_cap * (kQresMaxSplits + 1);
   if (need <= ix->ss_cap) return AHR_OK;
   if (ix->ss) AHR_HIP(hipFree(ix->ss));
@@ -3797,6 +3804,11 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   bool frag_done = false;
   if (pre_kernel == KERNEL_QRES) {
     if ((st = ensure_qbuf_kb(ix, s)) || (st = ensure_ss(ix, s))) return st;
+    // the whole batch after the previous register-resident batch of another stream (ahr_index::qres_done)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cap);
+    if (cap == hipStreamCaptureStatusNone && ix->qres_stream && ix->qres_stream != s)
+      AHR_HIP(hipStreamWaitEvent(s, ix->qres_done, 0));
     if (small_fuses_convert(ix)) {  // one launch: rows + fragments
       hipLaunchKernelGGL(convert_queries_frag_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B,
                          ix->dim, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, ix->dtype, ix->qbuf_kb,
@@ -3864,6 +3876,14 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
                       p.n_splits;
     launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
   }
+  if (p.kernel == KERNEL_QRES && ix->qres_done) {  // the next register-resident launch waits for this batch's merge
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cap);
+    if (cap == hipStreamCaptureStatusNone) {
+      AHR_HIP(hipEventRecord(ix->qres_done, s));
+      ix->qres_stream = s;
+    }
+  }
   prof_mark(ix, 4, s);
   if (ix->prof_calls < ix->prof_max_calls) ++ix->prof_calls;
   AHR_HIP(hipGetLastError());
@@ -3926,6 +3946,7 @@ int ahr_index_destroy(ahr_index* ix) {
     if (ix->parked[w].ss) (void)hipFree(ix->parked[w].ss);
   }
   for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
+  if (ix->qres_done) (void)hipEventDestroy(ix->qres_done);
   delete ix;
   return AHR_OK;
 }

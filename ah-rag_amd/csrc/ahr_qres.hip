@@ -85,11 +85,11 @@ static_assert(Cfg<12, 1>::kLds <= 160 * 1024 && Cfg<6, 1>::kLds <= 160 * 1024,
 // event: the selecting splits take the k-th largest published maxima (landed since the previous
 // event) as seeds, every split applies the seeds that landed, and both reads are issued again. The
 // first event (block 1, after the block-0 publication) waits, bounded, for every granule and seed.
-// From block 32 on (large corpora) the schedule continues every 8 blocks: a publication after block
-// 8m - 2 and an event at the end of block 8m - 1.
-constexpr uint32_t kSeedWaitTicks = 3000;  // s_memrealtime ticks (100 MHz): a 30-us bound per wait
+// From block 32 on (large corpora) the schedule continues every 8 blocks to block 127, then every
+// 128: a publication after block 8m - 2 (128m - 2) and an event at the end of block 8m - 1.
+constexpr uint32_t kSeedWaitTicks = 1000;  // s_memrealtime ticks (100 MHz): a 10-us bound per wait
 __device__ __forceinline__ bool in_sched(uint32_t mask, int bi, int off) {
-  return bi < 32 ? ((mask >> bi) & 1) != 0 : (bi + off) % 8 == 0;
+  return bi < 32 ? ((mask >> bi) & 1) != 0 : (bi + off) % (bi < 128 ? 8 : 128) == 0;
 }
 
 template <int CTRL, int ROW_MASK>

@@ -58,8 +58,8 @@ KERNEL_NAMES = {"lane256": "topk_lane_kernel", "lane256x128": "topk_lane_kernel"
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--workload", choices=["hotpot90k", "synth5m", "env"], default=None,
                     help="default: hotpot90k at N=1, synth5m (row-sharded) at N>1; env = configs[4], the RL "
                          "environment loop (VecAHRAGGymEnv, replicas: --envs per GPU)")
@@ -80,8 +80,9 @@ def parse_args(argv=None):
                     help="N=1 hotpot90k: skip the exact-mode (fp32 index) line beside the bf16 headline")
     ap.add_argument("--no-batch-sweep", action="store_true",
                     help="N=1 hotpot90k: skip the B = 1 and B = 64 lines beside the B = 1024 headline")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="batches in flight (one stream + index workspace each)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight (one stream + index workspace each); 0 = auto: 1 for the "
+                         "register-resident plan (it fills every CU and the library orders its batches), else 2")
     ap.add_argument("--recall-queries", type=int, default=256)
     ap.add_argument("--probe-seeds", action="store_true",
                     help="seed the fused kernels from a coarse-cluster probe (DenseIndex.build_clusters, built "
@@ -216,6 +217,12 @@ def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float,
     return out
 
 
+def auto_inflight(ix, B: int, k: int) -> int:
+    """Batches in flight for --inflight 0: one for the register-resident plan (its batches fill every
+    CU and the library orders them across streams, so a second gains nothing), else two."""
+    return 1 if ix.plan(B, k)["kernel"] == "qres256" else 2
+
+
 def time_queries(ix, q, k: int, steps: int, warmup: int, inflight: int, dev):
     """Queries/s of `ix` on batch q with `inflight` batches in flight (one stream + workspace
     each), then a serial pass with per-stage HIP events."""
@@ -336,7 +343,8 @@ def sub_line(args, dev, spec, dtype: str, workload: str, label: str) -> dict:
         ix.upsert(x, start=s0)
     q, _ = corpus.queries(B, rows, salt=0)
     steps = max(3, min(args.steps, 20))
-    dt, prof, res = time_queries(ix, q, k, steps, max(1, min(args.warmup, 3)), max(1, args.inflight), dev)
+    dt, prof, res = time_queries(ix, q, k, steps, max(1, min(args.warmup, 3)), args.inflight or auto_inflight(ix, B, k),
+                                 dev)
     calls = max(1, prof["calls"])
     tile_ms = prof["ms_sum"]["tile_topk"] / calls
     nq = min(128, B)
@@ -463,7 +471,7 @@ def run(args) -> None:
     # path; only the order of independent batches' kernels on the GPU changes.
     # Row-sharded runs pipeline the same way: batch i's RCCL all-gather and merge overlap batch
     # i + 1's local search (the collective is ordered after the work of the batch's stream).
-    inflight = max(1, args.inflight)
+    inflight = args.inflight if args.inflight > 0 else (1 if not sharded and auto_inflight(local, B, k) == 1 else 2)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(inflight - 1)]
     outs = [(torch.empty((B, k), dtype=torch.float32, device=dev), torch.empty((B, k), dtype=torch.int32, device=dev))
             for _ in range(inflight)]
@@ -485,8 +493,8 @@ def run(args) -> None:
                 return index.query(q, k, out_keys=keys[i])
             return local.query(q, k, out=outs[i])
 
-    def timed(depth: int) -> float:
-        for _ in range(args.warmup):
+    def timed(depth: int, warmup: int) -> float:
+        for _ in range(warmup):
             step(depth)
         torch.cuda.synchronize()
         if world > 1:
@@ -501,9 +509,11 @@ def run(args) -> None:
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    dt_serial = timed(1) if inflight > 1 else None
+    # (the serial pass comes first: it gets extra untimed warmup so the GPU is at its working clock)
+    dt_serial = timed(1, max(args.warmup, 200)) if inflight > 1 else None
     counter[0] = 0
-    dt = timed(inflight)
+    # (one batch in flight: no serial pass before it, so the same ramp to the working clock)
+    dt = timed(inflight, args.warmup if inflight > 1 else max(args.warmup, 200))
     local.set_workspace(0)
     res = step(1)
     torch.cuda.synchronize()
@@ -579,7 +589,7 @@ def run(args) -> None:
                 "parallelism": (f"rows{world}" if sharded else (f"queries{world}" if world > 1 else "single")),
                 "launch": plan,
                 "inflight": inflight,
-                "serial_ms_per_step": round(dt_serial / args.steps * 1e3, 4) if dt_serial else None,
+                "serial_ms_per_step": round((dt_serial or dt) / args.steps * 1e3, 4),
                 "recall_queries": nq,
                 "threshold_seed": (f"cluster probe ({clusters['clusters']} clusters, built in {clusters['build_s']} s)"
                                    if clusters else
@@ -600,7 +610,8 @@ def run(args) -> None:
             # scores bit-identical to the oracle's k-ordered fma chain), same corpus, queries, k
             f32 = DenseIndex(d, N, dtype="f32", device=dev)
             f32.upsert(rows)
-            f_dt, f_prof, f_res = time_queries(f32, q, k, args.steps, args.warmup, inflight, dev)
+            f_dt, f_prof, f_res = time_queries(f32, q, k, args.steps, args.warmup,
+                                               args.inflight or auto_inflight(f32, B, k), dev)
             f_tile = f_prof["ms_sum"]["tile_topk"] / max(1, f_prof["calls"])
             f_tf = 2.0 * B * N * d / (f_tile * 1e-3) / 1e12
             out["exact_fp32"] = {
@@ -620,7 +631,8 @@ def run(args) -> None:
             for b in (1, 64):
                 qb = q[:b].contiguous()
                 b_steps = args.steps * 4
-                b_dt, b_prof, _ = time_queries(local, qb, k, b_steps, args.warmup, inflight, dev)
+                b_dt, b_prof, _ = time_queries(local, qb, k, b_steps, args.warmup,
+                                               args.inflight or auto_inflight(local, b, k), dev)
                 b_calls = max(1, b_prof["calls"])
                 b_plan = local.plan(b, k)
                 entry = {
