@@ -142,6 +142,10 @@ __device__ __forceinline__ uint32_t wave_kth_grid(uint32_t v0, uint32_t v1, int 
   return t;
 }
 
+// the per-lane sorted list of the end phase (k <= 12; a 16-wide bitonic network in registers
+// measured 2.4 us slower at C2 than these insertions, which stop early on the partner's list)
+constexpr int kListCap = 12;
+
 __device__ __forceinline__ uint64_t granule_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: not from L1
 }
@@ -166,12 +170,12 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
 // threshold): pub[-1] holds this launch's tag (low 32 bits), advanced on the device by the query
 // conversion launched before it, so a replayed hipGraph gets a fresh one; then [256 qblocks]
 // [n_splits] published maxima, then [256 qblocks] seeds.
-template <int DT, int NKT, int SPB, int KCAP, int ABL>
+template <int DT, int NKT, int ABL>
 __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
     int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t sched) {
-  using C = Cfg<NKT, SPB>;
+  using C = Cfg<NKT, 1>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -246,7 +250,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     }
   };
 #pragma unroll
-  for (int st = 0; st < C::kAhead; ++st)
+  // the prologue fills every ring slot (stages 0 .. kAhead): the peeled first iteration then issues
+  // nothing, and block 0's chain waits on no stage but its own
+  for (int st = 0; st < C::kSlots; ++st)
     if (st < n_st) issue(st);
 
   // resident B fragments: step S of query q = bytes [32 S + 16 fh, +16) of its row
@@ -254,13 +260,15 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   {
     const uint8_t* src = qfrag + (int64_t)(qb * kWaves + wave) * C::kNS * 1024 + lane * 16;
 #pragma unroll
-    for (int S = 0; S < C::kNS; ++S) qf[S] = *reinterpret_cast<const u32x4*>(src + S * 1024);
+    for (int S = 0; S < C::kNS; ++S) {
+      qf[S] = *reinterpret_cast<const u32x4*>(src + S * 1024);
+      __builtin_amdgcn_sched_barrier(0);  // in step order: block 0's step S waits for fragment S only
+    }
   }
-  // The fragments and the seed are consumed here (one wait, behind the prologue DMA, both needed
-  // before the first MFMA anyway), so the loop never waits on them: a use inside the loop would
-  // make the waitcnt pass count the ring's in-flight pieces against them every stage.
-#pragma unroll
-  for (int S = 0; S < C::kNS; ++S) asm volatile("" : "+v"(qf[S]));
+  // The fragments stream in behind the prologue DMA and are consumed by block 0's chain, each
+  // waited for as its step needs it (the peeled first iteration below); after it an empty asm
+  // "consumes" them all, so the main loop never waits on them (a use inside the loop would make the
+  // waitcnt pass count the ring's in-flight pieces against them every stage).
   asm volatile("" : "+v"(thr));
   // (a score threshold only, no key: a score equal to it always passes, so exact ties may be
   // appended and cut again — correct, and the registers go to the resident fragments)
@@ -562,15 +570,37 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (ss && in_sched((uint32_t)sched, bi, 2)) publish();
   };
   stamp(2);
+  {  // iteration 0, peeled: the sync waits only for stage 0's pieces (the fragments are younger)
+    if (!(ABL & ABL_NOWAIT)) {  // younger than stage 0's pieces: the other prologue stages', the fragments
+      if (n_st >= 3 && C::kSlots == 3)
+        wait_vm<2 * C::kPPW + C::kNS>();
+      else if (n_st >= 2)
+        wait_vm<C::kPPW + C::kNS>();
+      else
+        wait_vm<C::kNS>();
+    }
+    if (!(ABL & ABL_NOBARRIER)) lds_barrier();
+    stamp(3);
+    if (live && n_st > 0) {
+      fa[0] = frag(0, 0);
+      fa[1] = frag(0, 1);
+      stage_mma(std::integral_constant<int, 0>{}, 0);
+    }
+#pragma unroll
+    for (int S = 0; S < C::kNS; ++S) asm volatile("" : "+v"(qf[S]));
+  }
 #pragma unroll 1
-  for (int j = 0; j <= n_st; ++j) {
+  for (int j = 1; j <= n_st; ++j) {
     stage_sync(j, young);
     young = 0;
     if (j <= 55) stamp(3 + j);
     const bool bend = j >= C::kSPB && j % C::kSPB == 0;  // block j / kSPB - 1 ended with stage j - 1
     const int bi = j / C::kSPB - 1;
     const bool first = ss && j == 2 * C::kSPB;  // uniform
-    if (j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2)) issue(j + C::kAhead);
+    // (at the first event the next stage is issued after it: its bounded polls then wait for their
+    // own reads only, not for a stage in flight)
+    const bool ring = j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2);  // (j >= 1: the prologue issued up to kAhead)
+    if (ring && !(first && live)) issue(j + C::kAhead);
     if (!live) continue;
     const bool mma = j < n_st;
     if (mma) {  // the stage's first fragments: in flight under the screening below
@@ -582,6 +612,10 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (bend && !first) finish_block(bi);
     if (ss && bend && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
     if (first) {
+      if (ring) {
+        issue(j + C::kAhead);
+        young = 0;  // the ring's pieces are the youngest now: the next sync waits for everything
+      }
       replay(b_begin * kTR);
       finish_block(bi);
     }
@@ -594,30 +628,30 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   }
 
   // this lane's buffered keys, sorted (the query registers are dead from here on)
-  uint64_t L[KCAP];
+  uint64_t L[kListCap];
 #pragma unroll
-  for (int j = 0; j < KCAP; ++j) L[j] = 0;
+  for (int j = 0; j < kListCap; ++j) L[j] = 0;
   uint64_t* const lbuf = lb();
 #pragma unroll 1
-  for (int c = 0; c < nb; ++c) list_insert<KCAP>(L, lbuf[c * kThreads]);
+  for (int c = 0; c < nb; ++c) list_insert<kListCap>(L, lbuf[c * kThreads]);
   // lane fr + 32 hands its list to lane fr through the (idle) ring
   __syncthreads();
-  uint64_t* xch = reinterpret_cast<uint64_t*>(smem) + (wave * 32 + fr) * KCAP;
+  uint64_t* xch = reinterpret_cast<uint64_t*>(smem) + (wave * 32 + fr) * kListCap;
   if (fh) {
 #pragma unroll
-    for (int j = 0; j < KCAP; ++j) xch[j] = L[j];
+    for (int j = 0; j < kListCap; ++j) xch[j] = L[j];
   }
   __syncthreads();
   if (!fh && q < n_q) {
 #pragma unroll 1
     for (int j = 0; j < k_out; ++j) {
       const uint64_t v = xch[j];
-      if (v <= L[KCAP - 1]) break;  // sorted: nothing further can enter
-      list_insert<KCAP>(L, v);
+      if (v <= L[kListCap - 1]) break;  // sorted: nothing further can enter
+      list_insert<kListCap>(L, v);
     }
     uint64_t* dst = part_keys + ((int64_t)q * n_splits + split) * k_out;
 #pragma unroll
-    for (int j = 0; j < KCAP; ++j)
+    for (int j = 0; j < kListCap; ++j)
       if (j < k_out) dst[j] = L[j];
   }
   stamp(62);
@@ -637,7 +671,7 @@ void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes
                      qfrag, epoch);
 }
 
-template <int DT, int NKT, int SPB, int KCAP, int ABL = 0>
+template <int DT, int NKT, int ABL = 0>
 void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, uint64_t* pub,
               uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
@@ -652,7 +686,7 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
       thr = reinterpret_cast<const float*>((uintptr_t)strtoull(e, nullptr, 16));
     }
 #define AHR_QRES_ABL(V) \
-  case V: launch_t<DT, NKT, SPB, KCAP, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
+  case V: launch_t<DT, NKT, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       AHR_QRES_ABL(32) AHR_QRES_ABL(64) AHR_QRES_ABL(128) AHR_QRES_ABL(192)
@@ -660,25 +694,13 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
     }
 #undef AHR_QRES_ABL
   }
-  constexpr auto kern = &topk_qres_kernel<DT, NKT, SPB, KCAP, ABL>;
+  constexpr auto kern = &topk_qres_kernel<DT, NKT, ABL>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  constexpr int lds = Cfg<NKT, SPB>::kLds;
+  constexpr int lds = Cfg<NKT, 1>::kLds;
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), lds, s, rows, qfrag,
                      row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub,
                      (pub_mask & 0xffffffffull) | (ev_mask << 32));
-}
-
-template <int DT, int NKT, int SPB>
-void launch_k(int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B,
-              uint32_t row_base, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags,
-              uint64_t* pub, uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
-  if (k <= 8)
-    launch_t<DT, NKT, SPB, 8>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags,
-                              pub, pub_mask, ev_mask, s);
-  else
-    launch_t<DT, NKT, SPB, 12>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks,
-                               flags, pub, pub_mask, ev_mask, s);
 }
 
 void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int d_pad_bytes,
@@ -687,8 +709,8 @@ void launch(int dtype, int k, const uint8_t* rows, const uint8_t* qfrag, int64_t
   const bool wide = d_pad_bytes == 12 * kRowBytes;
   pub_mask |= 1;  // block 0's maxima: the first event's sample
 #define AHR_QRES_L(D, N) \
-  launch_k<D, N, 1>(k, rows, qfrag, row_stride, n_rows, B, row_base, part_keys, thr, n_splits, qblocks, flags, pub, \
-                    pub_mask, ev_mask, s)
+  launch_t<D, N>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, \
+                 pub_mask, ev_mask, s)
   if (dtype == AHR_BF16) {
     if (wide)
       AHR_QRES_L(DT_BF16, 12);
