@@ -382,8 +382,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   unsigned char* const land = smem + C::kOffLand + wave * kLandBytes;
   if (tid % 64 < kLandBytes / 16) *reinterpret_cast<u32x4*>(land + lane * 16) = u32x4{0, 0, 0, 0};
   // The split selects for the queries j = split + m n_splits of its query block; the m-th goes to
-  // wave m % 8, so the selecting waves spread over the four SIMDs (waves w and w + 4 share one):
-  // a selection then runs beside the other wave's MFMA chain instead of stalling both.
+  // wave {0, 3, 5, 6, 1, 2, 4, 7}[m % 8], so any four consecutive ones sit on four different SIMDs
+  // whether a SIMD's two waves are w, w + 4 or 2s, 2s + 1 (measured: a selection still costs its
+  // block ~0.5 us, not hidden by the other wave's MFMA chain).
   // Per-lane table, built once (the divisions stay out of the loop): lane l < 32 of a wave, its
   // granule read (bit 31: a selecting lane; bits 24..29: its query i, the wave's i-th; bits 0..23:
   // the byte offset in the self-seeding buffer); lanes 48..52 the wave's count of selected queries,
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   if (ss) {
     const int ns = n_splits;
     const int np = ns >= 128 ? 32 : ns / 2;  // lanes per selected query
-    const int j0 = split + wave * ns;
+    const int j0 = split + ((0x73261540 >> (4 * wave)) & 7) * ns;  // m = {0, 4, 5, 1, 6, 2, 3, 7}[wave]
     int cnt = 0;
     for (int j = j0; j < kTQ && (int64_t)qb * kTQ + j < n_q; j += kWaves * ns) ++cnt;
     uint32_t e = 0;
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       landed(false);
       young = 0;  // everything this wave issued so far has completed
     }
-    if (!(ABL & ABL_EV_NOSEL) && cnt > 0) {  // the k-th largest of each selected query's published maxima
+    if ((first || !(ABL & ABL_EV_NOSEL)) && cnt > 0) {  // the k-th largest of each selected query's published maxima
       const u32x4 g = *reinterpret_cast<const u32x4*>(land + ln * 16);
       const uint32_t v0 = sel_lane && g[1] == epoch ? g[0] : 0u;
       const uint32_t v1 = sel_lane && g[3] == epoch ? g[2] : 0u;
@@ -479,9 +480,21 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     }
     apply_seed(*reinterpret_cast<const uint64_t*>(land + 512 + fr * 8));
     if constexpr (!(ABL & ABL_EV_NOISSUE)) {
-      issue_granules();  // for the next event
-      issue_seeds();
-      young += 2;
+      issue_granules();  // for the next event (its seeds are read one block later: seed_read)
+      ++young;
+    }
+  };
+  // The seed read of an event, one block after it: by then every selector of the query block has
+  // stored this round's seeds (read in the event itself, most would still be the previous round's).
+  auto seed_read = [&]() __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const u32x4 uni = *reinterpret_cast<const u32x4*>(tab + 48);
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(pub, (uint32_t)__builtin_amdgcn_readfirstlane((int)uni[2]));
+    const uint32_t seed_off = (uint32_t)__builtin_amdgcn_readfirstlane((int)uni[3]);
+    if constexpr (!(ABL & ABL_EV_NOISSUE)) {
+      if (ln < 16) blds16_pol(r, seed_off + 16 * ln, land + 512);
+      ++young;
     }
   };
   // block 0's raw scores parked in the upper half of the lane buffer (entries 8 .. 15, two floats
@@ -611,6 +624,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     // then runs with the first seed after block 0's parked scores)
     if (bend && !first) finish_block(bi);
     if (ss && bend && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
+    if (ss && bend && bi >= 3 && in_sched((uint32_t)(sched >> 32), bi - 1, 1)) seed_read();
     if (first) {
       if (ring) {
         issue(j + C::kAhead);
@@ -689,7 +703,8 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
   case V: launch_t<DT, NKT, V>(rows, qfrag, row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub, pub_mask, ev_mask, s); return;
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
-      AHR_QRES_ABL(32) AHR_QRES_ABL(64) AHR_QRES_ABL(128) AHR_QRES_ABL(192)
+      AHR_QRES_ABL(32) AHR_QRES_ABL(64) AHR_QRES_ABL(128) AHR_QRES_ABL(192) AHR_QRES_ABL(96) AHR_QRES_ABL(160)
+      AHR_QRES_ABL(224)
       default: break;
     }
 #undef AHR_QRES_ABL
