@@ -689,7 +689,7 @@ template <int DT, int NKT, int ABL = 0>
 void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int n_rows, int B, uint32_t row_base,
               int k, uint64_t* part_keys, const float* thr, int n_splits, int qblocks, int flags, uint64_t* pub,
               uint64_t pub_mask, uint64_t ev_mask, hipStream_t s) {
-  if constexpr (kAblation && ABL == 0 && DT == DT_BF16) {  // the profiling build: cost-split variants
+  if constexpr (kAblation && ABL == 0) {  // the profiling build: cost-split variants
     const int abl = ((flags & kFlagSkipEpilogue) ? ABL_NOSCREEN : 0) | ((flags & kFlagNoLoads) ? ABL_NOLOADS : 0) |
                     ((flags & kFlagNoWait) ? ABL_NOWAIT : 0) | ((flags & kFlagNoBarrier) ? ABL_NOBARRIER : 0) |
                     ((flags & kFlagNoLdsRead) ? ABL_NOREAD : 0) | ((flags & kFlagQresTrace) ? ABL_TRACE : 0) |

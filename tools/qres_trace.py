@@ -83,8 +83,11 @@ def main():
             "tail_us": round(float(np.median(us(t[:, 62]) - us(t[:, 3 + js]))), 3),
             "memtime_ticks_per_us": round(float(np.median(clk)), 1),
         }
+        # per workgroup (blockIdx order): exit relative to the first entry, for placement analyses
+        r["wg_exit_us"] = [round(float(x), 2) for x in us(t[:, 62])]
+        r["wg_entry_us"] = [round(float(x), 2) for x in us(t[:, 0])]
         out["reps"].append(r)
-        print(json.dumps(r))
+        print(json.dumps({kk: vv for kk, vv in r.items() if not kk.startswith("wg_")}))
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)
