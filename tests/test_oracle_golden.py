@@ -68,6 +68,47 @@ def test_search_cases(graph):
         assert search_ref.isclose_dicts(json.loads(json.dumps(got)), c["result"]), (c["query"], c["params"])
 
 
+def test_search_seeds_vs_numpy_f64(graph):
+    """The fixtures' dense step (R3) against an independent exhaustive scorer: numpy float64 matrix
+    products over the same stub-encoded vectors, not the C oracle the stand-in collection scored
+    with when the fixtures were made (tests/golden/make_golden.py), so the golden search results
+    are not anchored on the oracle alone. Every dense hit the reference recorded (result["seeds"],
+    return_cluster cases) must carry its f64 score within 1e-6 and lie in the f64 top-k (near-ties
+    within 1e-6 may trade places); unfiltered cases must return exactly the f64 top-k."""
+    G, meta = graph
+    cases = [c for c in _load("search_cases.json")["cases"] if c["return_cluster"]]
+    idx = _index(G)
+    idx_h = _index(G, include_hyperedges=True, indexed_meta=meta["vector_index"]["indexed_meta"])
+    filters = {"type_filter", "judge_overall_min", "confidence_min"}
+    n_checked = 0
+    for c in cases:
+        ids, vecs, _ = idx_h if c.get("include_hyperedges") else idx
+        if not ids:
+            continue
+        q = encoder_stub.encode([c["query"]], 384)[0].astype(np.float64)
+        s64 = vecs.astype(np.float64) @ q
+        p = search_ref.resolve_params(meta.get("search_params", {}), **c["params"])
+        k = min(p["top_k"], len(ids))
+        order = sorted(range(len(ids)), key=lambda i: (-s64[i], i))[:k]
+        kth = s64[order[-1]]
+        pos = {n: i for i, n in enumerate(ids)}
+        seeds = c["result"]["seeds"]
+        prev = np.inf
+        for sd in seeds:
+            r = pos[sd["node_id"]]
+            assert abs(sd["semantic"] - s64[r]) < 1e-6, (c["query"], sd["node_id"], sd["semantic"], s64[r])
+            assert s64[r] >= kth - 1e-6, (c["query"], sd["node_id"])
+            assert sd["semantic"] <= prev + 1e-6
+            prev = sd["semantic"]
+        if not (filters & set(c["params"])):
+            assert len(seeds) == k
+            got = sorted(pos[sd["node_id"]] for sd in seeds)
+            for r in set(got) ^ set(order):  # a row on one side only: a near-tie at the k-th score
+                assert abs(s64[r] - kth) < 1e-6, (c["query"], ids[r])
+        n_checked += 1
+    assert n_checked > 30
+
+
 def test_env_expansions(graph):
     G, _ = graph
     n = 0
