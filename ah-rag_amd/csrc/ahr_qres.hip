@@ -48,17 +48,16 @@ namespace ahr {
 namespace dense {
 namespace qres {
 
-// NKT 64-deep k-tiles per row (12 at d_pad 768, 6 at 384), SPB stages per 32-row block: a stage is
-// NKT / SPB k-tiles (24 KiB or a whole 48-KiB block). 24-KiB stages run a 3-slot ring issued two
-// stages ahead; 48-KiB stages a 2-slot ring issued one stage (a whole block) ahead.
+// NKT 64-deep k-tiles per row (12 at d_pad 768, 6 at 384); a ring stage is one whole 32-row block
+// (48 or 24 KiB). 24-KiB stages run a 3-slot ring issued two blocks ahead, 48-KiB stages a 2-slot
+// ring issued one block ahead.
 constexpr int kLandBytes = 768;
 static_assert(kPark >= 6, "the replay of a parked block never overtakes its unread quads");
 
-template <int NKT, int SPB>
+template <int NKT>
 struct Cfg {
-  static_assert(NKT % (6 * SPB) == 0, "stages of 6 or 12 k-tiles");
-  static constexpr int kSPB = SPB;                // stages per 32-row block
-  static constexpr int kSK = NKT / SPB;           // k-tiles per stage
+  static_assert(NKT == 6 || NKT == 12, "d_pad 384 or 768");
+  static constexpr int kSK = NKT;                 // k-tiles per stage (= block)
   static constexpr int kStage = kSK * kKt;        // 24 or 48 KiB
   static constexpr int kSlots = kSK == 12 ? 2 : 3;
   static constexpr int kAhead = kSlots - 1;       // stages in flight beyond the one multiplied
@@ -67,8 +66,7 @@ struct Cfg {
   static constexpr int kPPW = kPieces / kWaves;   // pieces per wave per stage
   static constexpr int kNS = NKT * 4;             // k16 steps = query fragments per lane
   static constexpr int kSS = kSK * 4;             // k16 steps per stage
-  // LDS: the ring, the seeding scratch (per wave 1 KiB: what of a seeding event's parked
-  // accumulators the free ring slot cannot hold; none with 48-KiB slots), the lane buffers
+  // LDS: the ring, the lane buffers, the landing zones, the event table
   static constexpr int kOffBuf = kSlots * kStage;
   // the seeding events' landing zone, per wave: 64 published maxima (512 B), 32 seeds (256 B)
   static constexpr int kOffLand = kOffBuf + kBufCap * kThreads * 8;
@@ -76,7 +74,7 @@ struct Cfg {
   static constexpr int kOffTab = kOffLand + kWaves * kLandBytes;
   static constexpr int kLds = kOffTab + kThreads * 4;
 };
-static_assert(Cfg<12, 1>::kLds <= 160 * 1024 && Cfg<6, 1>::kLds <= 160 * 1024,
+static_assert(Cfg<12>::kLds <= 160 * 1024 && Cfg<6>::kLds <= 160 * 1024,
               "LDS budget: one workgroup per CU");
 
 // Self-seeding schedule (uniform, over a split's block index; the host passes it, publications in
@@ -175,7 +173,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qfrag, int64_t row_stride, int n_rows, int n_q,
     uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys, const float* __restrict__ thr_init, int n_splits,
     int qblocks, int flags, uint64_t* __restrict__ pub, uint64_t sched) {
-  using C = Cfg<NKT, 1>;
+  using C = Cfg<NKT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -197,7 +195,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // control flow built on them scalar)
   const int b_begin = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n_blocks / n_splits));
   const int b_end = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n_blocks / n_splits));
-  const int n_st = C::kSPB * (b_end - b_begin);
+  const int n_st = b_end - b_begin;  // ring stages = blocks
   const int qw0 = qb * kTQ + wave * 32;
   const bool live = qw0 < n_q;  // wave-uniform: a wave past the batch only stages and syncs
   const int q = qw0 + fr;
@@ -234,9 +232,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   const uint32_t blk_bytes = (uint32_t)(kTR * row_stride);
   auto slot_of = [&](int st) __attribute__((always_inline)) { return smem + (st % C::kSlots) * C::kStage; };
   auto issue = [&](int st) __attribute__((always_inline)) {
-    const int b = b_begin + st / C::kSPB;
+    const int b = b_begin + st;
     const __amdgpu_buffer_rsrc_t r =
-        tile_rsrc(corpus + (int64_t)b * kTR * row_stride + (st % C::kSPB) * C::kSK * kRowBytes, blk_bytes);
+        tile_rsrc(corpus + (int64_t)b * kTR * row_stride, blk_bytes);
     unsigned char* slot = slot_of(st);
     int ln = lane;
     asm volatile("" : "+v"(ln));
@@ -548,19 +546,18 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   constexpr bool skip_screen = (ABL & ABL_NOSCREEN) != 0;
   f32x16 acc;
   u32x4 fa[3];
-  // the stage's 24 steps: step t prefetches step t + 2 and multiplies step t; H = stage of the block
-  auto stage_mma = [&](auto H, int st) __attribute__((always_inline)) {
-    constexpr int h = decltype(H)::value;
+  // a block's kSS k16 steps: step t prefetches step t + 2 and multiplies step t
+  auto stage_mma = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < C::kSS; ++t) {
       if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2);
       __builtin_amdgcn_sched_barrier(0);
-      if (h == 0 && t == 0) {
+      if (t == 0) {
         f32x16 z = {};
         mfma_step<DT>(fa[0], qf[0], z);
         acc = z;
       } else {
-        mfma_step<DT>(fa[t % 3], qf[h * C::kSS + t], acc);
+        mfma_step<DT>(fa[t % 3], qf[t], acc);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -597,7 +594,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (live && n_st > 0) {
       fa[0] = frag(0, 0);
       fa[1] = frag(0, 1);
-      stage_mma(std::integral_constant<int, 0>{}, 0);
+      stage_mma(0);
     }
 #pragma unroll
     for (int S = 0; S < C::kNS; ++S) asm volatile("" : "+v"(qf[S]));
@@ -607,9 +604,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     stage_sync(j, young);
     young = 0;
     if (j <= 55) stamp(3 + j);
-    const bool bend = j >= C::kSPB && j % C::kSPB == 0;  // block j / kSPB - 1 ended with stage j - 1
-    const int bi = j / C::kSPB - 1;
-    const bool first = ss && j == 2 * C::kSPB;  // uniform
+    const int bi = j - 1;  // the block that ended with stage j - 1
+    const bool first = ss && j == 2;  // uniform
     // (at the first event the next stage is issued after it: its bounded polls then wait for their
     // own reads only, not for a stage in flight)
     const bool ring = j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2);  // (j >= 1: the prologue issued up to kAhead)
@@ -622,9 +618,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     }
     // block bi's screening, then a seeding event (the first one before block 1's screening, which
     // then runs with the first seed after block 0's parked scores)
-    if (bend && !first) finish_block(bi);
-    if (ss && bend && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
-    if (ss && bend && bi >= 3 && in_sched((uint32_t)(sched >> 32), bi - 1, 1)) seed_read();
+    if (!first) finish_block(bi);
+    if (ss && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
+    if (ss && bi >= 3 && in_sched((uint32_t)(sched >> 32), bi - 1, 1)) seed_read();
     if (first) {
       if (ring) {
         issue(j + C::kAhead);
@@ -633,12 +629,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       replay(b_begin * kTR);
       finish_block(bi);
     }
-    if (mma) {
-      if (C::kSPB == 1 || !(j & 1))
-        stage_mma(std::integral_constant<int, 0>{}, j);
-      else
-        stage_mma(std::integral_constant<int, 1>{}, j);
-    }
+    if (mma) stage_mma(j);
   }
 
   // this lane's buffered keys, sorted (the query registers are dead from here on)
@@ -711,7 +702,7 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
   }
   constexpr auto kern = &topk_qres_kernel<DT, NKT, ABL>;
   static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  constexpr int lds = Cfg<NKT, 1>::kLds;
+  constexpr int lds = Cfg<NKT>::kLds;
   ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)(n_splits * qblocks)), dim3(kThreads), lds, s, rows, qfrag,
                      row_stride, n_rows, B, row_base, k, part_keys, thr, n_splits, qblocks, flags, pub,
