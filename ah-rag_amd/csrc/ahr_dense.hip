@@ -3638,7 +3638,7 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   // the register-resident kernel seeds itself (no pre-pass launch) unless kFlagQresPrepass asks for
   // the sampled pre-pass (A/B) or the caller supplies seeds
   const bool self_seed = p.kernel == KERNEL_QRES && S > 0 && !ix->seed && !(ix->debug_flags & kFlagQresPrepass) &&
-                         qres::self_seeds(ix->count, p.n_splits);
+                         qres::self_seeds(ix->count, p.n_splits, k);
   if (ix->seed) {
     thr = ix->seed;  // the caller's valid lower bounds of each query's k-th best score
   } else if (!self_seed && S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {

@@ -15,10 +15,13 @@ constexpr int kBufCap = 14;  // per-lane survivor buffer (keys) in LDS
 constexpr int kPark = kBufCap - 8;  // self-seeding: block 0's raw scores wait in entries kPark .. kBufCap - 1
 
 // Whether a launch seeds itself: every split has its first two blocks, the splits fit one wave's
-// selection (<= 128) and pair up in the landing zone (even). Otherwise the caller seeds it (the
-// pre-pass) or it runs unseeded.
-__host__ __device__ inline bool self_seeds(int64_t n_rows, int n_splits) {
-  return n_splits >= 2 && n_splits <= 128 && n_splits % 2 == 0 && (n_rows + kTR - 1) / kTR >= 2 * (int64_t)n_splits;
+// selection (<= 128), pair up in the landing zone (even), and are many enough for the k-th largest
+// of their maxima to be a useful bound (>= 32 and >= 2k: at 16 splits, B = 4096, the self-seeded
+// kernel measured 599 vs 493 us with the pre-pass; at 8 < k splits no seed exists at all).
+// Otherwise the caller seeds it (the pre-pass) or it runs unseeded.
+__host__ __device__ inline bool self_seeds(int64_t n_rows, int n_splits, int k) {
+  return n_splits >= 32 && n_splits >= 2 * k && n_splits <= 128 && n_splits % 2 == 0 &&
+         (n_rows + kTR - 1) / kTR >= 2 * (int64_t)n_splits;
 }
 
 // bf16 / f16 rows of d_pad_bytes = 1536 or 768 (d_pad = 768 or 384), k <= 12: what the kernel is built for.

@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   const int qw0 = qb * kTQ + wave * 32;
   const bool live = qw0 < n_q;  // wave-uniform: a wave past the batch only stages and syncs
   const int q = qw0 + fr;
-  const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && self_seeds(n_rows, n_splits);
+  const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && self_seeds(n_rows, n_splits, k_out);
   // ABL_TRACE (the profiling build only): thread 0 of each workgroup stamps into the buffer passed
   // as thr_init, 64 u64 per workgroup: [0] s_memrealtime at entry, [1] s_memtime at entry, [2] loop
   // entry, [3 + j] after stage j's sync (j <= 55), [59] first event entered, [60] selection done,

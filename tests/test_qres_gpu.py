@@ -63,7 +63,7 @@ def _check_forms(ix, Q, k):
     (40001, 700, 12, 8192, 384),
     (40001, 1024, 12, 0, 768),     # no seed: compaction from the first block on
     (33000, 2048, 8, 8192, 768),   # 32 splits
-    (33000, 4096, 10, 8192, 384),  # 16 splits: several first-round queries per wave, no later rounds
+    (33000, 4096, 10, 8192, 384),  # 16 splits: too few to seed itself, the pre-pass seeds it
     (5000, 600, 10, 0, 768),
     (5000, 600, 10, 8192, 768),    # 157 blocks over 80 splits: too few for self-seeding
     (300, 512, 5, 0, 768),         # 10 row blocks over 8 splits, queries 300.. of the second block dead
