@@ -41,7 +41,7 @@
 //   one coalesced 1-KiB load per wave per k16 step.
 // * Budget: NKT*16 query VGPRs + 16 accumulators + fragments in flight <= 256 (two waves per SIMD,
 //   one workgroup of 8 waves per CU); LDS at d_pad 768: 96 KiB ring + 56 KiB lane buffers + 6 KiB
-//   landing zones = 158 KiB.
+//   landing zones + 2 KiB event table = 160 KiB.
 #include "ahr_qres_common.h"
 
 namespace ahr {
@@ -495,10 +495,10 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       ++young;
     }
   };
-  // block 0's raw scores parked in the upper half of the lane buffer (entries 8 .. 15, two floats
+  // block 0's raw scores parked in the top of the lane buffer (entries kPark .. kPark + 7, two floats
   // each) until the first seed; replayed quad by quad from the bottom while the appends fill the
-  // buffer from entry 0: after quad qd at most 4 (qd + 1) keys, below entry 8 + 2 (qd + 1) — the
-  // appends never reach a quad not yet read.
+  // buffer from entry 0: after quad qd at most 4 (qd + 1) keys, below entry kPark + 2 (qd + 1)
+  // (kPark >= 6) — the appends never reach a quad not yet read.
   auto park = [&](const f32x16& acc) __attribute__((always_inline)) {
     uint64_t* const lbuf = lb();
 #pragma unroll
