@@ -632,13 +632,29 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     if (mma) stage_mma(j);
   }
 
-  // this lane's buffered keys, sorted (the query registers are dead from here on)
+  // this lane's buffered keys at or above its final threshold, sorted (the query registers are dead
+  // from here on). Entries appended while the seed was still loose stay buffered until a compaction;
+  // those below the final threshold (the last seed — read one block after the last event and not
+  // applied yet — or the lane's own k-th best) cannot be in the query's top k, since the threshold
+  // never exceeds the k-th best score. Dropping them first leaves a few inserts per lane instead of
+  // up to kBufCap (a wave runs as many as its fullest lane).
+  if (ss) {
+    wait_vm<0>();
+    asm volatile("" ::: "memory");
+    apply_seed(*reinterpret_cast<const uint64_t*>(land + 512 + fr * 8));
+  }
   uint64_t L[kListCap];
 #pragma unroll
   for (int j = 0; j < kListCap; ++j) L[j] = 0;
   uint64_t* const lbuf = lb();
+  int nk = 0;
 #pragma unroll 1
-  for (int c = 0; c < nb; ++c) list_insert<kListCap>(L, lbuf[c * kThreads]);
+  for (int c = 0; c < nb; ++c) {
+    const uint64_t v = lbuf[c * kThreads];
+    if (key_score(v) >= thr) lbuf[nk++ * kThreads] = v;
+  }
+#pragma unroll 1
+  for (int c = 0; c < nk; ++c) list_insert<kListCap>(L, lbuf[c * kThreads]);
   // lane fr + 32 hands its list to lane fr through the (idle) ring
   __syncthreads();
   uint64_t* xch = reinterpret_cast<uint64_t*>(smem) + (wave * 32 + fr) * kListCap;
