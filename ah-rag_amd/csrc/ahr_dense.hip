@@ -3117,13 +3117,15 @@ struct ahr_index {
   std::vector<hipEvent_t> prof_events;
   int prof_max_calls = 0;
   // The register-resident kernel fills every CU and its first seeding event waits (bounded) for
-  // every split: a batch of this plan on one workspace's stream launches that kernel after the
-  // previous batch's merge on another stream (qres_done), so no workgroup of another batch delays
-  // its start; its query conversion only waits for the previous batch's kernel (qres_kdone), so it
-  // runs beside that batch's merge.
+  // every split: a batch of this plan on one workspace's stream starts after the previous one's
+  // merge on another (its completion event), so no workgroup of another batch delays its start.
+  // The event is recorded only once batches of this plan have come on two streams (qres_multi): on
+  // one stream the order is the stream's own, and the record after the merge cost the serial C2
+  // step 4.7 us (merge stage 14.0 vs 9.3 us, profiles/r04/ab_endphase). (Two batches in flight
+  // gain nothing over one: bench.py runs this plan with one.)
   hipEvent_t qres_done = nullptr;
-  hipEvent_t qres_kdone = nullptr;
   hipStream_t qres_stream = nullptr;
+  bool qres_multi = false;
   int prof_calls = 0;
   uint32_t* fold_ctr() const { return reinterpret_cast<uint32_t*>(part + part_cap); }
 };
@@ -3257,7 +3259,6 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
 constexpr int64_t kQresMaxSplits = 256;
 int ensure_ss(ahr_index* ix, hipStream_t s) {
   if (!ix->qres_done) AHR_HIP(hipEventCreateWithFlags(&ix->qres_done, hipEventDisableTiming));
-  if (!ix->qres_kdone) AHR_HIP(hipEventCreateWithFlags(&ix->qres_kdone, hipEventDisableTiming));
   const int64_t need = 1 + ix->q_cap * (kQresMaxSplits + 1);
   if (need <= ix->ss_cap) return AHR_OK;
   if (ix->ss) AHR_HIP(hipFree(ix->ss));
@@ -3662,14 +3663,9 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       // self-seeding buffer: the tag (ss[0]), then [256 qblocks][n_splits] maxima and [256 qblocks] seeds
       const QresSchedule sch = qres_schedule();
       const bool once = (flags & kFlagQresSeedOnce) != 0;
-      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-      (void)hipStreamIsCapturing(s, &cap);
-      const bool order = cap == hipStreamCaptureStatusNone && ix->qres_done;
-      if (order && ix->qres_stream && ix->qres_stream != s) (void)hipStreamWaitEvent(s, ix->qres_done, 0);
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
                    p.n_splits, p.qblocks, (int)flags, self_seed ? ix->ss + 1 : nullptr, once ? 1 : sch.pub,
                    once ? 0 : sch.ev, s);
-      if (order) (void)hipEventRecord(ix->qres_kdone, s);  // the next batch's conversion waits for this
       return;
     }
     if (p.kernel == KERNEL_KB256) {
@@ -3812,12 +3808,13 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   bool frag_done = false;
   if (pre_kernel == KERNEL_QRES) {
     if ((st = ensure_qbuf_kb(ix, s)) || (st = ensure_ss(ix, s))) return st;
-    // the conversion after the previous register-resident batch's kernel on another stream, the
-    // kernel after that batch's merge (ahr_index::qres_done, waited in launch_search)
+    // the whole batch after the previous register-resident batch of another stream (ahr_index::qres_done)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cap);
-    if (cap == hipStreamCaptureStatusNone && ix->qres_stream && ix->qres_stream != s)
-      AHR_HIP(hipStreamWaitEvent(s, ix->qres_kdone, 0));
+    if (cap == hipStreamCaptureStatusNone && ix->qres_stream && ix->qres_stream != s) {
+      if (ix->qres_multi) AHR_HIP(hipStreamWaitEvent(s, ix->qres_done, 0));
+      ix->qres_multi = true;  // from the next batch on (this one's predecessor recorded nothing)
+    }
     if (small_fuses_convert(ix)) {  // one launch: rows + fragments
       hipLaunchKernelGGL(convert_queries_frag_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B,
                          ix->dim, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, ix->dtype, ix->qbuf_kb,
@@ -3889,7 +3886,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cap);
     if (cap == hipStreamCaptureStatusNone) {
-      AHR_HIP(hipEventRecord(ix->qres_done, s));
+      if (ix->qres_multi) AHR_HIP(hipEventRecord(ix->qres_done, s));
       ix->qres_stream = s;
     }
   }
@@ -3956,7 +3953,6 @@ int ahr_index_destroy(ahr_index* ix) {
   }
   for (hipEvent_t e : ix->prof_events) (void)hipEventDestroy(e);
   if (ix->qres_done) (void)hipEventDestroy(ix->qres_done);
-  if (ix->qres_kdone) (void)hipEventDestroy(ix->qres_kdone);
   delete ix;
   return AHR_OK;
 }
