@@ -279,9 +279,19 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     return lbuf0 + t;
   };
   int nb = 0;
-  // keep the k_out best buffered keys; the smallest kept is the lane's k-th best: new threshold
+  // keep the k_out best buffered keys at or above the threshold (seeds may have raised it since an
+  // entry was appended: those entries go in one pass); the smallest of k_out kept ones is the lane's
+  // k-th best: new threshold (fewer than k_out kept — k_out = 12 with 11 buffered, or after the
+  // pass — bound nothing)
   auto compact = [&]() {
     uint64_t* const lbuf = lb();
+    int nk = 0;
+#pragma unroll 1
+    for (int c = 0; c < nb; ++c) {
+      const uint64_t v = lbuf[c * kThreads];
+      if (key_score(v) >= thr) lbuf[nk++ * kThreads] = v;
+    }
+    nb = nk;
 #pragma unroll 1
     while (nb > k_out) {
       int mi = 0;
@@ -297,6 +307,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       lbuf[mi * kThreads] = lbuf[(nb - 1) * kThreads];
       --nb;
     }
+    if (nb < k_out) return;
     uint64_t mn = lbuf[0];
 #pragma unroll 1
     for (int c = 1; c < nb; ++c) {

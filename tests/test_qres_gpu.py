@@ -160,6 +160,42 @@ def test_qres_ties_order_by_row(cuda):
     ix.close()
 
 
+@pytest.mark.parametrize("prepass", [False, True])
+def test_qres_compaction_below_k(cuda, prepass):
+    """k = 12 and a lane buffer compacted while it holds 11 keys: a threshold taken from fewer than k
+    keys would exceed the lane's k-th best and drop the 12th. Query 0's 11 best rows all sit in one
+    lane's rows of one block (the lane's 16 rows of a 32-row block are block offsets 0-3, 8-11,
+    16-19, 24-27; 19 and 24-27 score low, so the next quad starts with 11 buffered keys and
+    compacts), its 12th best in the same lane one block later; the split's other rows score -1."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(71)
+    d, n, k = 768, 40000, 12
+    C = dr.normalize_rows(rng.standard_normal((n, d)).astype(np.float32))
+    Q = dr.normalize_rows(rng.standard_normal((1024, d)).astype(np.float32))
+    q0 = Q[0]
+
+    def at(cos):  # a unit row with cosine `cos` to q0
+        u = rng.standard_normal(d).astype(np.float32)
+        u -= (u @ q0) * q0
+        u /= np.linalg.norm(u)
+        return cos * q0 + np.sqrt(1 - cos * cos) * u
+
+    base = 39520  # block 5 of the last split (64 splits of 1,250 row blocks: rows 39,360..)
+    C[39360:] = -q0  # nothing else of that split enters the lane's buffer
+    for i, off in enumerate((0, 1, 2, 3, 8, 9, 10, 11, 16, 17, 18)):
+        C[base + off] = at(0.99 - 0.01 * i)
+    C[base + 32] = at(0.85)
+    ix = DenseIndex(d, n, dtype="bf16", device=cuda)
+    ix.upsert(C)
+    flags = QRES | (PREPASS if prepass else 0)
+    s, r = _run(ix, Q, k, flags, "qres256")
+    assert r[0, k - 1] == base + 32, r[0]
+    d_ = _run(ix, Q, k, TILELANE, "tilelane128")
+    np.testing.assert_array_equal(r, d_[1])
+    np.testing.assert_array_equal(s, d_[0])
+    ix.close()
+
+
 def test_qres_sharded_keys(cuda):
     """row_base offsets and the key merge through the register-resident plan == one unsharded query
     (the C4 shape in miniature)."""
