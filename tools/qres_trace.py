@@ -86,6 +86,11 @@ def main():
         # per workgroup (blockIdx order): exit relative to the first entry, for placement analyses
         r["wg_exit_us"] = [round(float(x), 2) for x in us(t[:, 62])]
         r["wg_entry_us"] = [round(float(x), 2) for x in us(t[:, 0])]
+        r["wg_clk"] = [round(float(x), 1) for x in clk]  # s_memtime ticks per us, per workgroup
+        x = np.arange(grid) & 7  # blockIdx -> XCD (round-robin dispatch)
+        r["xcd_exit_median_us"] = [round(float(np.median(us(t[x == i, 62]))), 2) for i in range(8)]
+        r["xcd_clk_median"] = [round(float(np.median(clk[x == i])), 1) for i in range(8)]
+        r["xcd_steady_block_us"] = [round(float(np.median(d[x == i, -10:-2])), 3) for i in range(8)]
         out["reps"].append(r)
         print(json.dumps({kk: vv for kk, vv in r.items() if not kk.startswith("wg_")}))
     if a.json:
