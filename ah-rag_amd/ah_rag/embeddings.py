@@ -335,7 +335,8 @@ class DenseIndex:
         1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
         1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768,
         k <= 12), 1 << 26 = that kernel seeded by the sampled pre-pass instead of seeding itself, 1 << 27 = its
-        self-seeding with the first event only.
+        self-seeding with the first event only, 1 << 28 / 1 << 19 = its splits XCD-balanced at any corpus
+        size / never (default: from 256 row blocks per split).
         Garbage-result cost-split switches (2, 256, 512, 1024, 1 << 20, 1 << 21, 1 << 24, 1 << 25)
         need the ablation build."""
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags) & 0xFFFFFFFF), "ahr_index_set_debug_flags")

@@ -2327,7 +2327,7 @@ __global__ __launch_bounds__(256) void convert_queries_frag_kernel(const float* 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && epoch) advance_epoch(epoch);  // the next qres launch's tag
+  if (blockIdx.x == 0 && threadIdx.x == 0 && epoch) advance_epoch_rebalance(epoch);  // the next qres launch's tag
   if (i >= n) return;
   convert_row_fast(src + i * dim, dim, normalize, dst + i * row_stride, d_pad, dt, lane, frag, i);
 }
@@ -3257,9 +3257,11 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
 // selection with no seed writes to; the kernel uses at most 128 splits, so they fit). Zeroed when allocated (tag 0 is never a
 // launch's), so a granule is only ever this workspace's own.
 constexpr int64_t kQresMaxSplits = 256;
+// ss[0..7]: the per-XCD row weights and duration sums (rebalance_xcds), ss[8]: the launch tag
+constexpr int64_t kQresTagOff = 8;
 int ensure_ss(ahr_index* ix, hipStream_t s) {
   if (!ix->qres_done) AHR_HIP(hipEventCreateWithFlags(&ix->qres_done, hipEventDisableTiming));
-  const int64_t need = 1 + ix->q_cap * (kQresMaxSplits + 1);
+  const int64_t need = kQresTagOff + 1 + ix->q_cap * (kQresMaxSplits + 1);
   if (need <= ix->ss_cap) return AHR_OK;
   if (ix->ss) AHR_HIP(hipFree(ix->ss));
   ix->ss = nullptr;
@@ -3657,14 +3659,19 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   }
   prof_mark(ix, 2, s);
   const int n = (int)ix->count;
-  const uint32_t flags = (p.xcd_remap ? kFlagXcdRemap : 0u) | ix->debug_flags;
+  // XCD-balanced splits on the register-resident plan from 256 row blocks per split (C3: 5M rows,
+  // 2,442 per split: 7.11-7.24 vs 7.35-7.50 ms per launch, same box; at C2's 44 no gain, the spread
+  // inside an XCD dominates there: profiles/r04/xcd_balance/)
+  const bool xcd_bal = p.kernel == KERNEL_QRES && p.xcd_remap && !(ix->debug_flags & kFlagNoXcdBalance) &&
+                       cdiv(ix->count, qres::kTR) >= 256 * (int64_t)p.n_splits;
+  const uint32_t flags = (p.xcd_remap ? kFlagXcdRemap : 0u) | (xcd_bal ? kFlagXcdBalance : 0u) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
     if (p.kernel == KERNEL_QRES) {
       // self-seeding buffer: the tag (ss[0]), then [256 qblocks][n_splits] maxima and [256 qblocks] seeds
       const QresSchedule sch = qres_schedule();
       const bool once = (flags & kFlagQresSeedOnce) != 0;
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
-                   p.n_splits, p.qblocks, (int)flags, self_seed ? ix->ss + 1 : nullptr, once ? 1 : sch.pub,
+                   p.n_splits, p.qblocks, (int)flags, self_seed ? ix->ss + kQresTagOff + 1 : nullptr, once ? 1 : sch.pub,
                    once ? 0 : sch.ev, s);
       return;
     }
@@ -3818,7 +3825,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     if (small_fuses_convert(ix)) {  // one launch: rows + fragments
       hipLaunchKernelGGL(convert_queries_frag_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B,
                          ix->dim, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, ix->dtype, ix->qbuf_kb,
-                         reinterpret_cast<uint32_t*>(ix->ss));
+                         reinterpret_cast<uint32_t*>(ix->ss + kQresTagOff));
       frag_done = true;
     }
   }
@@ -3827,7 +3834,8 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
                        (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                        ix->row_stride, ix->d_pad, ix->dtype);
   if (pre_kernel == KERNEL_QRES && !frag_done)
-    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, ix->qbuf_kb, reinterpret_cast<uint32_t*>(ix->ss), s);
+    qres::launch_frag(ix->qbuf, ix->row_stride, B, ix->d_pad * ix->elem, ix->qbuf_kb,
+                      reinterpret_cast<uint32_t*>(ix->ss + kQresTagOff), s);
   if (k > AHR_MAX_K) {
     switch (ix->dtype) {
       case AHR_BF16: return run_query_large_k<DT_BF16>(ix, B, k, (uint32_t)row_base, scores, rows, keys, s);

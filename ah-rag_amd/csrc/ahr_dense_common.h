@@ -135,6 +135,41 @@ __device__ __forceinline__ void advance_epoch(uint32_t* e) {
   *e = v ? v : 1u;
 }
 
+// Per-XCD row weights of the register-resident plan (XCD-balanced splits): the XCDs of one device
+// hold different clocks under this load (measured 1.93-2.01 GHz within one launch), so each launch's
+// splits get rows in proportion to the speed its XCD showed in the previous launch. w[0..7]: weights
+// (1024 = 1.0, 0 = not yet measured), w[8..15]: the previous launch's summed workgroup durations per
+// XCD (s_memrealtime ticks). Updated by the one thread that advances the launch tag, before the launch.
+constexpr uint32_t kXcdW = 1024, kXcdWMin = 820, kXcdWMax = 1280;
+__device__ __forceinline__ void rebalance_xcds(uint32_t* w) {
+  uint32_t* t = w + 8;
+  bool all = true;
+  float mean = 0.f;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    all = all && t[x] != 0u;
+    mean += (float)t[x] * 0.125f;
+  }
+  if (all) {  // new weight ~ old weight x (mean duration / own duration), renormalised to 1024 on average
+    float v[8], sum = 0.f;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      v[x] = (float)(w[x] ? w[x] : kXcdW) * mean / (float)t[x];
+      sum += v[x];
+    }
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+      w[x] = (uint32_t)fminf(fmaxf(v[x] * (8.f * kXcdW) / sum, (float)kXcdWMin), (float)kXcdWMax);
+  }
+#pragma unroll
+  for (int x = 0; x < 8; ++x) t[x] = 0u;
+}
+// the tag advance of a register-resident launch; its weights sit 8 u64 before the tag
+__device__ __forceinline__ void advance_epoch_rebalance(uint32_t* e) {
+  advance_epoch(e);
+  rebalance_xcds(reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(e) - 8));
+}
+
 // Workgroup barrier that waits for this wave's LDS traffic but leaves global_load_lds in flight
 // (__syncthreads() would emit vmcnt(0) and drain the ring).
 __device__ __forceinline__ void lds_barrier() {
@@ -200,6 +235,8 @@ enum : uint32_t {
   kFlagNoLdsRead = 1u << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
   kFlagQresPrepass = 1u << 26,   // qres kernel seeded by the sampled pre-pass launch, not by itself (A/B)
   kFlagQresSeedOnce = 1u << 27,  // qres self-seeding: the first event only, no later rounds (A/B)
+  kFlagXcdBalance = 1u << 28,    // qres: XCD-balanced splits at any corpus size (default from 256 row blocks per split)
+  kFlagNoXcdBalance = 1u << 19,  // qres: equal splits at any corpus size (A/B)
   kFlagQresTrace = 1u << 29,  // qres kernel: per-workgroup timestamps into AHR_QRES_TRACE_PTR (ablation build)
   kFlagQresEvNoSel = 1u << 30,   // qres seeding events without the selection (wrong seeds: ablation build)
   kFlagQresEvNoIssue = 1u << 31, // qres seeding events without the landing reads (ablation build)
@@ -218,7 +255,7 @@ constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagN
                                        kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead | kFlagQresTrace |
                                        kFlagQresEvNoSel | kFlagQresEvNoIssue;
 constexpr uint32_t kKnownFlags = kKernelFlags | kWrongResultFlags | kFlagNoTilePrefetch | kFlagNoFold |
-                                 kFlagQresPrepass | kFlagQresSeedOnce;
+                                 kFlagQresPrepass | kFlagQresSeedOnce | kFlagXcdBalance | kFlagNoXcdBalance;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 }  // namespace dense

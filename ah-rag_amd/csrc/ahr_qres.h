@@ -37,7 +37,8 @@ void launch_frag(const uint8_t* qbuf, int64_t row_stride, int B, int d_pad_bytes
 
 // One fused launch: part_keys [B][n_splits][k] (the merge kernels' input), thr [B] optional
 // admission seeds. grid = n_splits * qblocks; n_splits % 8 == 0 when flags has the XCD remap bit.
-// pub: the self-seeding buffer, nullptr for none: pub[-1] = the launch's tag (low 32 bits), which
+// pub: the self-seeding buffer, nullptr for none: pub[-9 .. -2] = the per-XCD row weights and
+// duration sums (rebalance_xcds), pub[-1] = the launch's tag (low 32 bits), which
 // the query conversion stream-ordered before this launch advanced (no earlier launch on these
 // buffers used it); then [256 qblocks][n_splits] published maxima, then [256 qblocks] seeds.
 // pub_mask / ev_mask: the self-seeding schedule over a split's block index (bit bi: publish the

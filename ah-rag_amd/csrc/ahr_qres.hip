@@ -153,7 +153,7 @@ __device__ __forceinline__ void granule_store(uint64_t* p, uint64_t v) {
 __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ qbuf, int64_t row_stride, int64_t n16,
                                                    int ns, uint8_t* __restrict__ qfrag, uint32_t* __restrict__ epoch) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 16-B chunk of the output
-  if (i == 0 && epoch) advance_epoch(epoch);
+  if (i == 0 && epoch) advance_epoch_rebalance(epoch);
   if (i >= n16) return;
   const int l = (int)(i & 63);
   const int64_t gs = i >> 6;
@@ -191,15 +191,37 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     qb = blockIdx.x / n_splits;
   }
   const int n_blocks = (n_rows + kTR - 1) / kTR;
-  // (64-bit divisions run on the VALU: readfirstlane keeps the loop bounds, the stage index and the
-  // control flow built on them scalar)
-  const int b_begin = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n_blocks / n_splits));
-  const int b_end = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n_blocks / n_splits));
-  const int n_st = b_end - b_begin;  // ring stages = blocks
   const int qw0 = qb * kTQ + wave * 32;
   const bool live = qw0 < n_q;  // wave-uniform: a wave past the batch only stages and syncs
   const int q = qw0 + fr;
   const bool ss = pub != nullptr && (ABL & ABL_NOSCREEN) == 0 && self_seeds(n_rows, n_splits, k_out);
+  // XCD-balanced splits (kFlagXcdBalance, self-seeding launches with the XCD remap: split s runs on
+  // XCD s mod 8): the splits of XCD x get rows in proportion to its weight (rebalance_xcds, set from
+  // the previous launch's durations before this one); the bounds stay a partition of the blocks,
+  // >= 2 blocks per split (weights within 0.64x-1.56x of each other, >= 4 blocks per split on average)
+  uint32_t* const xcdw = ss ? reinterpret_cast<uint32_t*>(pub - 9) : nullptr;
+  const bool bal = ss && (flags & kFlagXcdRemap) && (flags & kFlagXcdBalance) && n_splits % 8 == 0 &&
+                   n_blocks >= 4 * n_splits;
+  // (64-bit divisions run on the VALU: readfirstlane keeps the loop bounds, the stage index and the
+  // control flow built on them scalar)
+  int b_begin, b_end;
+  if (bal) {
+    int64_t W = 0, pre = 0, own = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const int64_t w = xcdw[x] ? xcdw[x] : kXcdW;
+      W += w;
+      pre += x < (split & 7) ? w : 0;
+      own = x == (split & 7) ? w : own;
+    }
+    const int64_t c0 = (int64_t)(split >> 3) * W + pre, tot = (int64_t)(n_splits >> 3) * W;
+    b_begin = __builtin_amdgcn_readfirstlane((int)(c0 * n_blocks / tot));
+    b_end = __builtin_amdgcn_readfirstlane((int)((c0 + own) * n_blocks / tot));
+  } else {
+    b_begin = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n_blocks / n_splits));
+    b_end = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n_blocks / n_splits));
+  }
+  const int n_st = b_end - b_begin;  // ring stages = blocks
   // ABL_TRACE (the profiling build only): thread 0 of each workgroup stamps into the buffer passed
   // as thr_init, 64 u64 per workgroup: [0] s_memrealtime at entry, [1] s_memtime at entry, [2] loop
   // entry, [3 + j] after stage j's sync (j <= 55), [59] first event entered, [60] selection done,
@@ -424,6 +446,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     }
     tab[lane] = e;
   }
+  // this workgroup's start, for its XCD's duration sum (lane 60 of wave 0's table row is spare)
+  if (bal && tid == 0) tab[60] = (uint32_t)__builtin_amdgcn_s_memrealtime();
   auto event_site = [&](bool first) __attribute__((always_inline)) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
@@ -686,6 +710,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     for (int j = 0; j < kListCap; ++j)
       if (j < k_out) dst[j] = L[j];
   }
+  if (bal && tid == 0)
+    __hip_atomic_fetch_add(xcdw + 8 + (split & 7), (uint32_t)__builtin_amdgcn_s_memrealtime() - tab[60],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(62);
   stamp(63, true);
 }

@@ -160,6 +160,24 @@ def test_qres_ties_order_by_row(cuda):
     ix.close()
 
 
+def test_qres_xcd_balanced_splits(cuda):
+    """XCD-balanced splits (flag 1 << 28): the split bounds move with the per-XCD weights each
+    launch sets for the next; every launch must still cover every row once — bitwise the tile
+    kernel's answer, launch after launch as the weights settle."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(83)
+    C = _clustered(rng, 90000, 768)
+    Q = _clustered(rng, 1024, 768)
+    ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ref = _run(ix, Q, 10, TILELANE, "tilelane128")
+    for _ in range(6):
+        s, r = _run(ix, Q, 10, QRES | (1 << 28), "qres256")
+        np.testing.assert_array_equal(r, ref[1])
+        np.testing.assert_array_equal(s, ref[0])
+    ix.close()
+
+
 @pytest.mark.parametrize("prepass", [False, True])
 def test_qres_compaction_below_k(cuda, prepass):
     """k = 12 and a lane buffer compacted while it holds 11 keys: a threshold taken from fewer than k
