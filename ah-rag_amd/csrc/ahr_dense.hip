@@ -3251,8 +3251,9 @@ bool qres_ok(const ahr_index* ix, int B, int k) {
   return B >= kQresMinBatch && sample_rows_for(ix) > 0 && ix->count >= kQresMinRows;
 }
 
-// Self-seeding buffer of the register-resident plan (ahr_qres.hip): the launch tag (advanced on the
-// device by each query conversion), then per query slot of the padded batch one published maximum
+// Self-seeding buffer of the register-resident plan (ahr_qres.hip): the per-XCD row weights and
+// duration sums (kQresTagOff words), the launch tag (advanced on the device by each query
+// conversion), then per query slot of the padded batch one published maximum
 // per split (at most kQresMaxSplits), then one seed (and, past the seeds, the spare slots a
 // selection with no seed writes to; the kernel uses at most 128 splits, so they fit). Zeroed when allocated (tag 0 is never a
 // launch's), so a granule is only ever this workspace's own.
@@ -3667,7 +3668,8 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   const uint32_t flags = (p.xcd_remap ? kFlagXcdRemap : 0u) | (xcd_bal ? kFlagXcdBalance : 0u) | ix->debug_flags;
   if constexpr (DT != DT_F32) {
     if (p.kernel == KERNEL_QRES) {
-      // self-seeding buffer: the tag (ss[0]), then [256 qblocks][n_splits] maxima and [256 qblocks] seeds
+      // self-seeding buffer: the per-XCD weights and duration sums (ss[0..7]), the tag (ss[8]), then
+      // [256 qblocks][n_splits] maxima and [256 qblocks] seeds
       const QresSchedule sch = qres_schedule();
       const bool once = (flags & kFlagQresSeedOnce) != 0;
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
