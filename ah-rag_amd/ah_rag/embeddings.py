@@ -328,18 +328,23 @@ class DenseIndex:
 
     def set_debug_flags(self, flags: int) -> None:
         """Plan / A/B switches (include/ahr.h; a 32-bit unsigned word, unknown bits refused):
-        8 = 128x128 tile kernel (cooperative), 32 = 128x128 lane-local kernel at any batch,
-        2048 = plan without the query-resident kernels, 4096 = the query-resident (qkv) kernel
-        wherever it applies, 16384 = tilelane without the cross-tile prefetch, 32768 = the 256x256
+        4 = the register-resident kernel's split 0 seeds under a tag no launch has (its bounded
+        waits time out; results unchanged: a test of that path), 8 = 128x128 tile kernel
+        (cooperative), 32 = 128x128 lane-local kernel at any batch, 2048 = plan without the
+        query-resident kernels, 4096 = the 128-query-resident (qkv) kernel wherever it applies (the
+        ablation build only), 16384 = tilelane without the cross-tile prefetch, 32768 = the 256x256
         16x16x32 kernel (bf16/f16, k <= 16), 131072 / 262144 = always / never the k-blocked kernel,
         1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
         1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768,
         k <= 12), 1 << 26 = that kernel seeded by the sampled pre-pass instead of seeding itself, 1 << 27 = its
         self-seeding with the first event only, 1 << 28 / 1 << 19 = its splits XCD-balanced at any corpus
         size / never (default: from 256 row blocks per split).
-        Garbage-result cost-split switches (2, 256, 512, 1024, 1 << 20, 1 << 21, 1 << 24, 1 << 25)
-        need the ablation build."""
-        nat.check(nat.lib().ahr_index_set_debug_flags(self._h, int(flags) & 0xFFFFFFFF), "ahr_index_set_debug_flags")
+        Garbage-result cost-split switches (2, 256, 512, 1024, 1 << 20, 1 << 21, 1 << 24, 1 << 25,
+        1 << 29 .. 1 << 31) need the ablation build. Values outside [0, 2**32) raise ValueError."""
+        flags = int(flags)
+        if not 0 <= flags < 1 << 32:
+            raise ValueError(f"debug flags must fit an unsigned 32-bit word, got {flags}")
+        nat.check(nat.lib().ahr_index_set_debug_flags(self._h, flags), "ahr_index_set_debug_flags")
 
     _KERNELS = ("tile128", "lane256", "(retired)", "tilelane128", "(retired)", "qkv128", "t256", "small", "kb256",
                 "(retired)", "qres256")

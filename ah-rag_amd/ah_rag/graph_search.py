@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from . import devtime
 from .embeddings import _on_stream
 
 EDGE_TYPES = ("belongs_to", "related_to", "participates_in")
@@ -190,7 +191,7 @@ class DeviceGraph:
         cnt = torch.empty((B,), dtype=torch.int32, device=dev)
         x = inputs.to(device=dev, dtype=torch.int32).contiguous()
         _on_stream(stream, dev, x, out, cnt)
-        with torch.cuda.device(dev):
+        with torch.cuda.device(dev), devtime.span(stream, dev):
             nat.check(nat.lib().ahr_graph_lca(self._h, nat.ptr(x), B, n_in, int(max_out), nat.ptr(out), nat.ptr(cnt),
                                               nat.stream_ptr(stream)), "ahr_graph_lca")
         return out, cnt
@@ -233,7 +234,7 @@ class DeviceGraph:
         cnt = torch.empty((B,), dtype=torch.int32, device=dev)
         x = inputs.to(device=dev, dtype=torch.int32).contiguous()
         _on_stream(stream, dev, x, out, cnt)
-        with torch.cuda.device(dev):
+        with torch.cuda.device(dev), devtime.span(stream, dev):
             nat.check(nat.lib().ahr_graph_expand(self._h, ACTIONS[action], nat.ptr(x), B, n_in, int(limit),
                                                  nat.ptr(out), nat.ptr(cnt), nat.stream_ptr(stream)),
                       "ahr_graph_expand")
@@ -335,13 +336,14 @@ class SearchEngine:
         # rows past the index count come back as -1 anyway: ask for at most count (Chroma's
         # n_results clamp), so a small corpus answers any top_k
         k_dense = min(k, max(1, len(self.index)), nat.AHR_MAX_K_LARGE)
-        scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
-        if stream is not None:  # the gather below and the host copies run on the current stream
-            torch.cuda.current_stream(self.graph.device).wait_stream(stream)
-        valid = rows >= 0
-        nodes = torch.where(valid, self.row_to_node[rows.clamp_min(0).long()], torch.full_like(rows, -1))
-        res = self.graph.expand_rerank(nodes, scores, params, stream=stream)
-        if stream is not None:
-            torch.cuda.current_stream(self.graph.device).wait_stream(stream)
+        with devtime.span(None, self.graph.device):  # (recorded on the current stream, after the waits)
+            scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
+            if stream is not None:  # the gather below and the host copies run on the current stream
+                torch.cuda.current_stream(self.graph.device).wait_stream(stream)
+            valid = rows >= 0
+            nodes = torch.where(valid, self.row_to_node[rows.clamp_min(0).long()], torch.full_like(rows, -1))
+            res = self.graph.expand_rerank(nodes, scores, params, stream=stream)
+            if stream is not None:
+                torch.cuda.current_stream(self.graph.device).wait_stream(stream)
         host = res.to_host()
         return rows.cpu().numpy(), scores.cpu().numpy(), host

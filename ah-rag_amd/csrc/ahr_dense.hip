@@ -3199,6 +3199,7 @@ inline int sample_rows_for(const ahr_index* ix) {
 }
 
 bool qkv_ok(const ahr_index* ix, int B, int k) {
+  if (!kAblation) return false;  // compiled into the ablation build only (round 5)
   const int nkt = ix->d_pad * ix->elem / kRowBytes;
   if (k > 16 || ix->dtype == AHR_F32 || !(nkt == 6 || nkt == 12)) return false;
   if (ix->debug_flags & (kFlagTile128 | kFlagTileLane | kFlagNoQres)) return false;
@@ -3240,15 +3241,24 @@ bool kb256_ok(const ahr_index* ix, int B, int k) {
 // (kFlagQres) or keep it out (kFlagNoQres, or any other kernel flag).
 constexpr int kQresMinBatch = 512;
 constexpr int64_t kQresMinRows = 32768;
+// the register-resident plan's splits: one wave of 256 workgroups; a multiple of 8 with the XCD remap
+// (>= 8 splits), else every split the grid has room for (fewer than 8 never seed themselves anyway)
+inline int qres_splits(int64_t count, int B) {
+  int want = std::max(1, 256 / (int)cdiv(B, qres::kTQ));
+  want = (int)std::min<int64_t>(want, std::max<int64_t>(1, cdiv(count, qres::kTR)));
+  return want >= 8 ? want / 8 * 8 : want;
+}
 bool qres_ok(const ahr_index* ix, int B, int k) {
   if (!qres::supported(ix->dtype, ix->d_pad * ix->elem, k) || B <= 0) return false;
   if (ix->debug_flags & kFlagNoQres) return false;
   if (ix->debug_flags & kFlagQres) return true;
   if (ix->debug_flags & kForceFlags) return false;  // another kernel explicitly requested
-  // (also past kKB256MinRows, where the corpus streams from HBM: 5M x 768 f16, B = 1024, self-seeded
-  // qres256 6.96 ms vs kb256 7.45 ms per launch on the same box, profiles/r04/ab_sched/c3; round 3's
-  // pre-pass-seeded two-stage form was behind, 7.71 vs 7.49)
-  return B >= kQresMinBatch && sample_rows_for(ix) > 0 && ix->count >= kQresMinRows;
+  if (B < kQresMinBatch || sample_rows_for(ix) <= 0 || ix->count < kQresMinRows) return false;
+  // Past kKB256MinRows (the corpus streams from HBM) only where the launch seeds itself: 5M x 768
+  // f16, B = 1024, self-seeded qres256 6.96 ms vs kb256 7.45 ms per launch on the same box
+  // (profiles/r04/ab_sched/c3); the pre-pass-seeded form (B >= 4096: <= 16 splits) was measured
+  // behind kb256 (round 3 at B = 1024: 7.71 vs 7.49 ms), so those batches keep kb256.
+  return ix->count < kKB256MinRows || qres::self_seeds(ix->count, qres_splits(ix->count, B), k);
 }
 
 // Self-seeding buffer of the register-resident plan (ahr_qres.hip): the per-XCD row weights and
@@ -3311,10 +3321,8 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.kernel = KERNEL_QRES;
     p.qblocks = (int)cdiv(B, qres::kTQ);
     p.n_row_tiles = (int)cdiv(ix->count, qres::kTR);
-    int want = std::max(1, 256 / p.qblocks);
-    want = std::min(want, std::max(1, p.n_row_tiles));
-    p.xcd_remap = want >= 8;
-    p.n_splits = p.xcd_remap ? want / 8 * 8 : std::max(1, want & ~1);  // even: self-seeding pairs splits
+    p.n_splits = qres_splits(ix->count, B);
+    p.xcd_remap = p.n_splits >= 8;
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     return p;
   }
@@ -3695,13 +3703,15 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
         launch_t256<DT, 16>(ix, p, n, B, k, row_base, thr, flags, s);
       return;
     }
-    if (p.kernel == KERNEL_QKV) {
+#ifdef AHR_ABLATION
+    if (p.kernel == KERNEL_QKV) {  // (the ablation build only: qkv_ok plans it nowhere else)
       if (ix->d_pad * ix->elem / kRowBytes == 12)
         launch_qkv_k<DT, 12>(ix, p, n, B, k, row_base, thr, flags, s);
       else
         launch_qkv_k<DT, 6>(ix, p, n, B, k, row_base, thr, flags, s);
       return;
     }
+#endif
   }
   if (p.kernel == KERNEL_TILELANE) {
     switch (k <= 8 ? 8 : (k <= 12 ? 12 : 16)) {  // lists sized to k

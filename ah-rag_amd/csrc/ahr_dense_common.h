@@ -216,13 +216,15 @@ enum { MODE_TOPK = 0, MODE_GROUPMAX = 1, MODE_SCORES = 2 };
 enum : uint32_t {
   kFlagXcdRemap = 1,
   kFlagSkipEpilogue = 2,  // GEMM only: the top-k epilogue is skipped (wrong results)
+  kFlagQresMute = 4,      // qres self-seeding: split 0's seeding traffic carries another launch's tag, so every
+                          // bounded wait on it times out (a test of the timeout path; results unchanged)
   kFlagTile128 = 8,       // the 128x128 tile kernel with cooperative screening, any k
   kFlagTileLane = 32,     // the 128x128 lane-local kernel at any batch (k <= 16)
   kFlagMaxOnly = 256,     // lane kernel: group maxima only, no scan (wrong results)
   kFlagNoLoads = 512,     // tile kernel: operands loaded for the first tile only (wrong results)
   kFlagNoWait = 1024,     // tilelane kernel: loads issued but never waited for (wrong results)
   kFlagNoQres = 2048,     // plan without the query-resident kernels (qkv and qres)
-  kFlagQkv = 4096,        // the query-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 16)
+  kFlagQkv = 4096,        // the 128-query-resident kernel wherever it applies (ablation build only)
   kFlagNoTilePrefetch = 16384,  // tilelane: each tile's k-tile 0 issued at the tile start (ablation)
   kFlagT256 = 32768,      // the 256x256 16x16x32 kernel wherever it applies (bf16/f16, k <= 16)
   kFlagKB256 = 131072,    // the k-blocked 256x256 kernel wherever it applies (bf16/f16, k <= 16)
@@ -254,8 +256,10 @@ constexpr uint32_t kForceFlags = kKernelFlags & ~(kFlagNoQres | kFlagNoKB256);
 constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagNoLoads | kFlagNoWait | kFlagTileZero |
                                        kFlagTileFirst | kFlagNoBarrier | kFlagNoLdsRead | kFlagQresTrace |
                                        kFlagQresEvNoSel | kFlagQresEvNoIssue;
-constexpr uint32_t kKnownFlags = kKernelFlags | kWrongResultFlags | kFlagNoTilePrefetch | kFlagNoFold |
-                                 kFlagQresPrepass | kFlagQresSeedOnce | kFlagXcdBalance | kFlagNoXcdBalance;
+// (the 128-query-resident kernel, kFlagQkv, is compiled into the ablation build only)
+constexpr uint32_t kKnownFlags = (kKernelFlags & (kAblation ? ~0u : ~(uint32_t)kFlagQkv)) | kWrongResultFlags |
+                                 kFlagNoTilePrefetch | kFlagNoFold | kFlagQresPrepass | kFlagQresSeedOnce |
+                                 kFlagXcdBalance | kFlagNoXcdBalance | kFlagQresMute;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
 }  // namespace dense

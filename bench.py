@@ -60,10 +60,15 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--workload", choices=["hotpot90k", "synth5m", "env"], default=None,
-                    help="default: hotpot90k at N=1, synth5m (row-sharded) at N>1; env = configs[4], the RL "
+    ap.add_argument("--workload", choices=["hotpot90k", "hotpot90k_d384", "synth5m", "env"], default=None,
+                    help="default: hotpot90k at N=1, synth5m (row-sharded) at N>1; hotpot90k_d384 = the same "
+                         "corpus at the reference's default width d = 384; env = configs[4], the RL "
                          "environment loop (VecAHRAGGymEnv, replicas: --envs per GPU)")
     ap.add_argument("--envs", type=int, default=1024, help="--workload env: environments per GPU")
+    ap.add_argument("--episodes", type=int, default=5, help="C5 line: timed episodes after a warm-up one")
+    ap.add_argument("--clock-ramp", type=int, default=200,
+                    help="untimed steps before the --warmup steps of the timed pass (the GPU reaches its working "
+                         "clock; reported as config.clock_ramp_steps)")
     ap.add_argument("--no-sublines", action="store_true",
                     help="N=1 hotpot90k: skip the synth5m (configs[2]) and C5 env (configs[4]) sub-lines")
     ap.add_argument("--batch", type=int, default=1024)
@@ -109,6 +114,32 @@ def numpy_topk(corpus: np.ndarray, queries: np.ndarray, k: int, row_base: int = 
     for b in range(s.shape[0]):
         idx[b] = part[b][np.lexsort((part[b], -ps[b]))]
     return np.take_along_axis(s, idx, axis=1), idx.astype(np.int64) + row_base
+
+
+def cpu_baseline_chunked(chunks, queries: np.ndarray, k: int, n_rows: int, d: int):
+    """(exact top-k rows, cpu_baseline) over a corpus too large to build twice: each chunk is
+    brought to host memory untimed, then the reference math (fp32 BLAS Q @ C.T + argpartition, the
+    running top-k merged with the tie rule) is timed on it with all of the process's BLAS threads.
+    The sample is the queries given over the whole corpus."""
+    info = host_info()
+    best_s = np.full((len(queries), k), -np.inf, np.float32)
+    best_r = np.full((len(queries), k), -1, np.int64)
+    t_cpu = 0.0
+    for s0, x in chunks:
+        xh = np.ascontiguousarray(x.cpu().numpy())
+        t0 = time.perf_counter()
+        cs, cr = numpy_topk(xh, queries, k, row_base=s0)
+        alls, allr = np.concatenate([best_s, cs], 1), np.concatenate([best_r, cr], 1)
+        order = np.lexsort((allr, -alls), axis=1)[:, :k]
+        best_s, best_r = np.take_along_axis(alls, order, 1), np.take_along_axis(allr, order, 1)
+        t_cpu += time.perf_counter() - t0
+    cpu = {"value": round(len(queries) / t_cpu, 2), "unit": "queries/s", "cores": info.get("blas_threads", 1),
+           "kind": "port",
+           "sample": (f"{len(queries)} queries of the batch over the full {n_rows}x{d} fp32 corpus (host-resident "
+                      f"chunks; only the host math timed), numpy BLAS ({info.get('blas', 'unknown')}, "
+                      f"{info.get('blas_threads')} threads) + argpartition top-{k} + running merge, {t_cpu:.1f}s"),
+           "host": info}
+    return best_r, cpu
 
 
 def numpy_topk_chunked(chunks, queries: np.ndarray, k: int):
@@ -215,6 +246,69 @@ def cpu_baseline(rows: np.ndarray, queries: np.ndarray, k: int, budget_s: float,
     out["sample"] = sample + f"; host {json.dumps(info)}"
     out["host"] = info
     return out
+
+
+def _dense_topk(vectors: np.ndarray, q: np.ndarray, k: int):
+    """The reference's dense step on the host at B = 1 (one Chroma query per env reset,
+    hierarchical_graph.py:714), restated as numpy fp32 BLAS + argpartition, ties by row."""
+    s = vectors @ q
+    part = np.argpartition(-s, k - 1)[:k]
+    order = part[np.lexsort((part, -s[part]))]
+    return s[order], order
+
+
+def cpu_env_baseline(hg, ids, vectors: np.ndarray, qv: np.ndarray, steps: int, budget_s: float = 10.0,
+                     seed: int = 20251003) -> dict:
+    """configs[4] on the host: the reference's environment loop (policy_ppo.py:163-214: every env
+    reset, then stepped one after another), restated by the oracle (oracle/search_ref.py: the
+    search() tail expand_rerank of hierarchical_graph.py:719-789, GymEpisode for environment.py:
+    118-150, :301-355, :393-480 and gym_env.py:41-125) over the same networkx graph, with the dense
+    top-5 of each reset as numpy fp32 BLAS over the same 90k x d fp32 vectors. Random valid actions
+    as in the GPU line. Timed twice for half the budget each: with the graph's node/edge counts
+    computed once, and recounted for every observation as the reference does (environment.py:
+    136-139). `value` is the faster (counted-once) form."""
+    from oracle import search_ref  # CPU baseline leg only
+    G = hg.G
+    p = search_ref.resolve_params(G.graph.get("search_params", {}), top_k=5, member_top_m=5)
+    metas = {}
+
+    def meta(nid):
+        m = metas.get(nid)
+        if m is None:
+            m = metas[nid] = hg._embedding_text(nid)[1]
+        return m
+
+    def run(per_obs: bool, budget: float):
+        rng = np.random.default_rng(seed)
+        # one environment object reset per episode (policy_ppo.py:145 builds the envs once)
+        ep = search_ref.GymEpisode(G, max_steps=steps + 1, counts_per_observation=per_obs)
+        n_steps, i, t0 = 0, 0, time.perf_counter()
+        while True:
+            sc, rows = _dense_topk(vectors, qv[i % len(qv)], 5)
+            dist = (np.float32(1.0) - sc.astype(np.float32)).tolist()
+            seeds = [{"node_id": ids[r], "semantic": 1.0 - float(x), "meta": meta(ids[r])} for r, x in zip(rows, dist)]
+            ep.reset(search_ref.expand_rerank(G, seeds, p, return_cluster=True))
+            n_steps += 1
+            for _ in range(steps):
+                ep.step(int(rng.choice(np.flatnonzero(np.asarray(ep.mask())))))
+                n_steps += 1
+            i += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget:
+                return n_steps, i, dt
+
+    info = host_info()
+    s_once, e_once, t_once = run(False, budget_s / 2)
+    s_obs, e_obs, t_obs = run(True, budget_s / 2)
+    return {"value": round(s_once / t_once, 1), "unit": "env-steps/s", "cores": info.get("blas_threads", 1),
+            "kind": "port",
+            "reference_counts_per_observation_env_steps_per_s": round(s_obs / t_obs, 1),
+            "sample": (f"{e_once} episodes (reset + {steps} random valid steps) stepped one env after another over the "
+                       f"{G.number_of_nodes()}-node networkx graph, dense top-5 by numpy fp32 BLAS "
+                       f"({info.get('blas', 'unknown')}, {info.get('blas_threads')} threads; the rest single-threaded "
+                       f"Python) over {vectors.shape[0]}x{vectors.shape[1]}, {t_once:.1f}s; with the reference's "
+                       f"per-observation node/edge recount: {e_obs} episodes, {t_obs:.1f}s"),
+            "host": info}
 
 
 def auto_inflight(ix, B: int, k: int) -> int:
@@ -348,9 +442,15 @@ def sub_line(args, dev, spec, dtype: str, workload: str, label: str) -> dict:
     calls = max(1, prof["calls"])
     tile_ms = prof["ms_sum"]["tile_topk"] / calls
     nq = min(128, B)
-    _, exact = numpy_topk_chunked(chunks(), q[:nq].cpu().numpy(), k)
     plan = ix.plan(B, k)
     ix.close()
+    cpu = None
+    if rows is None and not args.no_cpu_baseline:
+        # the corpus is generated chunk by chunk: the recall ground truth and the CPU baseline come
+        # from one pass, with only the host work on each host-resident chunk timed
+        exact, cpu = cpu_baseline_chunked(chunks(), q[:nq].cpu().numpy(), k, N, d)
+    else:
+        _, exact = numpy_topk_chunked(chunks(), q[:nq].cpu().numpy(), k)
     return {
         "workload": label,
         "value": round(B * steps / dt, 1), "unit": "queries/s", "steps": steps,
@@ -359,6 +459,7 @@ def sub_line(args, dev, spec, dtype: str, workload: str, label: str) -> dict:
         "launch": plan,
         "stages_ms_per_step": {kk: round(v / calls, 4) for kk, v in prof["ms_sum"].items()},
         "roofline": roofline(plan, dtype, B, N, d, k, tile_ms, workload),
+        "cpu_baseline": cpu,
     }
 
 
@@ -367,8 +468,11 @@ def env_line(args, dev, rank: int = 0, world: int = 1) -> dict:
     130k-node HotpotQA-shaped graph, `--envs` environments per GPU, plus the drop-in single-env rate."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_env  # noqa: E402
+    cpu_fn = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu_fn = lambda *x: cpu_env_baseline(*x, budget_s=max(4.0, args.cpu_seconds))  # noqa: E731
     return bench_env.measure(dev, args.envs, 6, single=32, rank=rank, world=world, total_envs=args.envs * world,
-                             backend=args.backend)
+                             backend=args.backend, episodes=max(1, args.episodes), cpu_baseline_fn=cpu_fn)
 
 
 def run_env(args) -> None:
@@ -390,12 +494,12 @@ def run_env(args) -> None:
         steps = r["steps_per_episode"] + 1  # the reset counts as one env step, as in the rate
         out = {
             "metric": r["metric"], "value": r["vec_env_steps_per_s"], "unit": "env-steps/s", "n_gpus": world,
-            "steps": steps, "warmup": steps, "ms_per_step": round(r["episode_s"] / steps * 1e3, 4),
+            "steps": steps * r["episodes"], "warmup": steps, "ms_per_step": round(r["episode_s"] / steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": r["data"],
             "config": {"workload": "env: BASELINE configs[4], 2-hop expand + re-score inside the RL env loop",
                        "envs_per_gpu": r["envs_per_gpu"], "parallelism": r["parallelism"], "graph": r["graph"]},
-            "c5": r, "roofline": None, "cpu_baseline": None,
+            "c5": r, "roofline": None, "cpu_baseline": r.get("cpu_baseline"),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -424,8 +528,8 @@ def run(args) -> None:
         else:
             dist.init_process_group("gloo")
 
-    spec = HOTPOT_90K if workload == "hotpot90k" else SYNTH_5M
-    dtype = args.dtype or ("bf16" if workload == "hotpot90k" else "f16")
+    spec = {"hotpot90k": HOTPOT_90K, "hotpot90k_d384": HOTPOT_90K_D384}.get(workload, SYNTH_5M)
+    dtype = args.dtype or ("f16" if workload == "synth5m" else "bf16")
     B, k = args.batch, args.k
     corpus = SyntheticCorpus(spec, dev)
     N, d = spec.n_rows, spec.dim
@@ -509,11 +613,11 @@ def run(args) -> None:
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    # (the serial pass comes first: it gets extra untimed warmup so the GPU is at its working clock)
-    dt_serial = timed(1, max(args.warmup, 200)) if inflight > 1 else None
+    # (the serial pass comes first: it gets the clock ramp, so the GPU is at its working clock)
+    dt_serial = timed(1, args.clock_ramp + args.warmup) if inflight > 1 else None
     counter[0] = 0
-    # (one batch in flight: no serial pass before it, so the same ramp to the working clock)
-    dt = timed(inflight, args.warmup if inflight > 1 else max(args.warmup, 200))
+    # (one batch in flight: no serial pass before it, so the ramp precedes the --warmup steps here)
+    dt = timed(inflight, args.warmup if inflight > 1 else args.clock_ramp + args.warmup)
     local.set_workspace(0)
     res = step(1)
     torch.cuda.synchronize()
@@ -583,12 +687,17 @@ def run(args) -> None:
             "data": "synthetic (SURVEY.md §8d clustered generator, seed 20251003; no HotpotQA/encoder offline)",
             "recall_at_10": round(rec, 4),
             "config": {
-                "workload": ("hotpot90k: HotpotQA-distractor-shaped corpus 87k entity + 3k summary rows"
-                             if workload == "hotpot90k" else "synth5m: 5M-row synthetic corpus"),
+                "workload": {"hotpot90k": "hotpot90k: HotpotQA-distractor-shaped corpus 87k entity + 3k summary rows",
+                             "hotpot90k_d384": "hotpot90k_d384: the hotpot90k corpus at d = 384"}.get(
+                                 workload, "synth5m: 5M-row synthetic corpus"),
                 "corpus_rows": N, "dim": d, "batch": B, "top_k": k, "index_dtype": dtype,
                 "parallelism": (f"rows{world}" if sharded else (f"queries{world}" if world > 1 else "single")),
                 "launch": plan,
                 "inflight": inflight,
+                # untimed steps run before the --warmup steps of a timed pass (the step is ~0.15 ms: the
+                # GPU's clock settles over the first few ms of load); warmup + clock_ramp_steps ran untimed
+                "clock_ramp_steps": args.clock_ramp,
+                "untimed_steps_before_timed_region": args.clock_ramp + args.warmup,
                 "serial_ms_per_step": round((dt_serial or dt) / args.steps * 1e3, 4),
                 "recall_queries": nq,
                 "threshold_seed": (f"cluster probe ({clusters['clusters']} clusters, built in {clusters['build_s']} s)"

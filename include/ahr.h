@@ -125,30 +125,35 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
                          void* stream);
 
 /* Kernel-selection switches (A/B measurements; results stay correct), a 32-bit unsigned flag word:
- * 8 = always the 128x128 tile kernel with cooperative screening, 32 = the 128x128 lane-local tile
- * kernel at any batch (k <= 16), 2048 = no query-resident kernel (qkv or qres256), 4096 = the
- * query-resident kernel (qkv) wherever it applies, 16384 = tilelane without the cross-tile
- * prefetch, 32768 = the 256x256 16x16x32 kernel, 131072 = the k-blocked 256x256 kernel wherever it
- * applies, 262144 = never the k-blocked kernel, 1 << 22 = small batches merge through a merge
- * launch instead of the last-workgroup fold, 1 << 23 = the 256-query register-resident kernel
- * (qres256) wherever it applies (bf16/f16, d_pad 384 or 768, k <= 12), 1 << 26 = qres256 seeded
- * by the sampled pre-pass launch instead of seeding itself, 1 << 27 = qres256's self-seeding with
- * its first event only (no later rounds).
- * Cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
+ * 4 = qres256's split 0 seeds under a tag no launch has, so every bounded seeding wait on it runs
+ * to its time limit (a test of that path), 8 = always the 128x128 tile kernel with cooperative
+ * screening, 32 = the 128x128 lane-local tile kernel at any batch (k <= 16), 2048 = no
+ * query-resident kernel (qkv or qres256), 16384 = tilelane without the cross-tile prefetch, 32768 =
+ * the 256x256 16x16x32 kernel, 131072 = the k-blocked 256x256 kernel wherever it applies, 262144 =
+ * never the k-blocked kernel, 1 << 19 = qres256 splits never XCD-balanced, 1 << 22 = small batches
+ * merge through a merge launch instead of the last-workgroup fold, 1 << 23 = the 256-query
+ * register-resident kernel (qres256) wherever it applies (bf16/f16, d_pad 384 or 768, k <= 12),
+ * 1 << 26 = qres256 seeded by the sampled pre-pass launch instead of seeding itself, 1 << 27 =
+ * qres256's self-seeding with its first event only (no later rounds), 1 << 28 = qres256 splits
+ * XCD-balanced at any corpus size (default: from 256 row blocks per split).
+ * Accepted only by the ablation build (-DAHR_ABLATION, __graft_entry__.build_ablation; the shipped
+ * library returns AHR_EUNSUP): 4096 = the 128-query-resident kernel (qkv) wherever it applies, and
+ * the cost-split switches that give WRONG results (2 = skip the top-k epilogue, 256 = group maxima
  * only, 512 = operands of the first tile only, 1024 = loads never waited for, 1048576 / 2097152 =
  * k-blocked tiles read from tile 0 / the split's first tile, 1 << 24 / 1 << 25 = qres256 without
- * stage barriers / LDS fragment reads) are accepted only by the ablation
- * build (-DAHR_ABLATION, __graft_entry__.build_ablation); the shipped library returns AHR_EUNSUP.
+ * stage barriers / LDS fragment reads, 1 << 29 = qres256 per-workgroup timestamps, 1 << 30 /
+ * 1 << 31 = qres256 seeding events without the selection / without the landing reads).
  * Unknown bits return AHR_EINVAL. */
 int ahr_index_set_debug_flags(ahr_index* ix, uint32_t flags);
 
 /* Launch geometry the next query of batch B, top-k would use (diagnostics / bench reporting).
  * *kernel: 0 = 128x128 tile kernel (cooperative screening; k > 16), 1 = 256x256 lane kernel
  * (k <= 16, B >= 6144), 3 = 128x128 lane-local tile kernel (k <= 16, B < 6144), 5 = query-resident
- * kernel (opt-in), 6 = 256x256 16x16x32 kernel (opt-in), 7 = small-batch streaming kernel
+ * kernel (ablation build only), 6 = 256x256 16x16x32 kernel (opt-in), 7 = small-batch streaming kernel
  * (bf16/f16, B <= 16, k <= 16), 8 = k-blocked 256x256 kernel (bf16/f16, k <= 16, from 512k corpus
- * rows), 10 = 256-query register-resident kernel (bf16/f16, d_pad 384 or 768, k <= 12, B >= 512,
- * 32k to 512k rows, self-seeded). Ids 2, 4 and 9 are retired. */
+ * rows, below the register-resident kernel's batches), 10 = 256-query register-resident kernel
+ * (bf16/f16, d_pad 384 or 768, k <= 12, B >= 512, from 32k rows; from 512k rows only where it seeds
+ * itself: >= 32 splits, i.e. B <= 2048). Ids 2, 4 and 9 are retired. */
 int ahr_index_plan(const ahr_index* ix, int B, int k, int* kernel, int* n_splits, int* tiles_per_split,
                    int* qblocks);
 
@@ -159,7 +164,11 @@ int ahr_index_reserve(ahr_index* ix, int max_batch, int max_k);
  * ahr_index_query_keys / ahr_index_reserve calls use: the converted queries, per-split partial
  * lists and pre-pass buffers. Calls on different workspaces may run concurrently on different
  * streams (a serving loop keeping several batches in flight); calls on one workspace must be
- * ordered on one stream. No reference counterpart (the reference is one synchronous call). */
+ * ordered on one stream. Exception: batches of the register-resident plan (kernel id 10) fill every
+ * CU and their first seeding event waits (bounded) for every split, so the library serializes them
+ * across streams itself (each waits for the previous such batch's merge on another stream); under
+ * hipGraph capture that cross-stream ordering is not recorded (the captured graph orders its own
+ * batches). No reference counterpart (the reference is one synchronous call). */
 int ahr_index_set_workspace(ahr_index* ix, int slot);
 
 /* Replaces coll.query(query_embeddings=[q], n_results=k) (hierarchical_graph.py:714), batched.

@@ -269,11 +269,22 @@ class GymEpisode:
     TOP = {0: 2, 1: 2, 2: 1, 3: 3, 4: 1}
     EXPAND = {0: "parents", 1: "children", 2: "related"}
 
-    def __init__(self, G: nx.DiGraph, max_steps: int = 6, repeat_penalty: float = 0.02) -> None:
+    def __init__(self, G: nx.DiGraph, max_steps: int = 6, repeat_penalty: float = 0.02,
+                 counts_per_observation: bool = False) -> None:
+        """counts_per_observation: recount the graph's nodes and edges for every observation, as the
+        reference does (environment.py:136-139, an O(N) networkx walk per call; the host baseline of
+        bench.py's C5 line times both forms); False: counted once (same values)."""
         self.G = G
-        self.counts = {"n_nodes": G.number_of_nodes(), "n_edges": G.number_of_edges()}
+        self._counts_once = {"n_nodes": G.number_of_nodes(), "n_edges": G.number_of_edges()}
+        self.counts_per_observation = bool(counts_per_observation)
         self.max_steps = max(1, int(max_steps))
         self.repeat_penalty = float(repeat_penalty)
+
+    @property
+    def counts(self) -> Dict[str, int]:
+        if self.counts_per_observation:
+            return {"n_nodes": self.G.number_of_nodes(), "n_edges": self.G.number_of_edges()}
+        return self._counts_once
 
     def _brief_scored(self, res: Dict[str, Any]) -> Dict[str, Any]:
         b = node_brief(self.G, res.get("node_id"))

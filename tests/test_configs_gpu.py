@@ -9,9 +9,12 @@ C2  hotpot90k: 90,000 x 768 (87k entity + 3k summary rows, SURVEY §8d generator
     rows equal numpy's fp32 `Q @ C.T` + argpartition top-10 except near-ties (the two fp32
     accumulation orders differ by a few ulps; a swap is allowed only where the double-precision
     scores of the swapped rows are within 1e-5 of each other).
-C3  synth5m: 5,000,000 x 768 fp16, B = 1024, top-10: a sampled subset of 64 queries is checked
-    against the oracle over the fp16-rounded corpus (chunked through host memory), same
-    tolerances as C2 bf16.
+C2 at d = 384 (the reference's default all-MiniLM-L6-v2 width, hierarchical_graph.py:50, 603, 705):
+    the same corpus generator at 90,000 x 384, B = 1024, bf16, every query against the f64 oracle
+    with the C2 bf16 tolerances.
+C3  synth5m: 5,000,000 x 768 fp16, B = 1024, top-10: a sampled subset of 256 queries (a quarter of
+    the batch: every query block and split of the default plan) is checked against the oracle over
+    the fp16-rounded corpus (chunked through host memory), same tolerances as C2 bf16.
 
 References: the dense step replaces coll.query, /root/reference/src/ah_rag/graph/
 hierarchical_graph.py:714 (exhaustive-cosine restatement: oracle/ahr_oracle.c).
@@ -90,6 +93,23 @@ def test_c2_bf16_default_plan(hotpot, cuda):
     m = _check_half(s, r, Cr, Qr, es, er)
     _log_margin("c2_bf16_default_plan", batch=B, k=K, kernel=plan["kernel"], **m)
     assert m["rows_differing"] <= B * K // 1000  # near-ties are rare (documented in DESIGN.md §4)
+
+
+def test_c2_d384_bf16_default_plan(cuda):
+    """The C2 workload at the reference's default embedding width (d = 384): rows and scores of
+    every query against the f64 oracle on the storage-rounded inputs, the near-tie rule of
+    _check_half, margins logged."""
+    from ah_rag.synthetic import CorpusSpec, SyntheticCorpus
+    corpus = SyntheticCorpus(CorpusSpec(dim=384), cuda)
+    rows = corpus.rows()
+    q, _ = corpus.queries(B, rows)
+    (s, r), plan = _query("bf16", rows, q, cuda, expect_kernel="qres256")
+    C, Q = rows.cpu().numpy(), q.cpu().numpy()
+    Cr, Qr = dr.round_to_storage(C, "bf16"), dr.round_to_storage(Q, "bf16")
+    es, er = dr.topk(Cr, Qr, K, mode="f64")
+    m = _check_half(s, r, Cr, Qr, es, er)
+    _log_margin("c2_d384_bf16_default_plan", batch=B, k=K, dim=384, kernel=plan["kernel"], **m)
+    assert m["rows_differing"] <= B * K // 1000
 
 
 def test_c2_f32_bit_exact(hotpot, cuda):
@@ -191,7 +211,7 @@ def test_c3_synth5m_f16_sampled(cuda):
     s, r = s.cpu().numpy(), r.cpu().numpy().astype(np.int64)
     ix.close()
     assert plan["kernel"] in ("qres256", "kb256"), plan  # the defaults at 5M rows (B >= 512 / below)
-    pick = np.random.default_rng(11).choice(B, 64, replace=False)
+    pick = np.sort(np.random.default_rng(11).choice(B, 256, replace=False))
     Qr = dr.round_to_storage(qh.numpy()[pick], "f16")
     # oracle over the whole corpus, chunk by chunk (top-k of the union = top-k of chunk top-ks)
     best_s = np.full((len(pick), K), -np.inf)
@@ -215,6 +235,10 @@ def test_c3_synth5m_f16_sampled(cuda):
         ex = np.array([[Qr[i].astype(np.float64) @ rows_h[int(got_r[i, j])] for j in range(K)]
                        for i in range(len(pick))])
         assert (np.abs(ex[mism] - best_s[mism]) < 2e-5).all()
+    gap = float(np.abs(ex[mism] - best_s[mism]).max()) if mism.any() else 0.0
+    _log_margin("c3_synth5m_f16_sampled", batch=B, k=K, sampled_queries=len(pick), kernel=plan["kernel"],
+                rows_differing=int(mism.sum()), queries_differing=int(mism.any(axis=1).sum()),
+                max_exact_gap_at_differing_rank=gap, max_score_err_vs_f64=float(np.abs(got_s - best_s).max()))
     # known-answer half: perturbed corpus rows should mostly find their source row
     hits = [int(src[i]) in set(r[i].tolist()) for i in range(B // 2)]
     assert np.mean(hits) > 0.95
@@ -224,7 +248,8 @@ def test_c3_synth5m_f16_sampled(cuda):
 def test_c4_synth5m_row_shards_bitwise(cuda, G):
     """C4 (BASELINE configs[3]): the 5M x 768 f16 corpus row-sharded G ways exactly as
     ShardedDenseIndex shards it (rank g owns [g*N/G, (g+1)*N/G), row_base = lo_g), every shard
-    answered by its own DenseIndex in this process (2.5M / 1.25M / 625k rows: the kb256 plan), the
+    answered by its own DenseIndex in this process (2.5M / 1.25M / 625k rows: the self-seeded qres256
+    plan at B = 1024), the
     [B, G, k] key lists merged on the device (ahr_topk_merge, what follows the RCCL all-gather):
     the merged keys must equal the unsharded 5M answer bit for bit (scores, rows, tie order). The
     unsharded answer itself is checked against the oracle by test_c3_synth5m_f16_sampled."""

@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 QRES = 1 << 23      # plan the register-resident kernel wherever it applies
 PREPASS = 1 << 26   # ... seeded by the sampled pre-pass launch instead of by itself
 TILELANE = 32       # the lane-local 128x128 tile kernel at any batch
+MUTE = 4            # split 0 seeds under a tag no launch has: every bounded wait on it times out
 T256 = 32768        # the 256x256 16x16x32 tile kernel
 
 
@@ -330,4 +331,58 @@ def test_qres_reserve_allocates_nothing(cuda):
     ref = [t.cpu().numpy() for t in ix.query(Q, 10)]
     np.testing.assert_array_equal(out[1].cpu().numpy(), ref[1])
     np.testing.assert_array_equal(out[0].cpu().numpy(), ref[0])
+    ix.close()
+
+
+@pytest.mark.parametrize("d,n,B,k", [(768, 90000, 1024, 10), (384, 90000, 1024, 10), (768, 40001, 2048, 12)])
+def test_qres_seed_wait_timeouts(cuda, d, n, B, k):
+    """The bounded waits of the self-seeding (ahr_qres.hip: the first event polls up to 10 us for
+    every split's block-0 granule, then for its queries' seeds) must only weaken the seed when
+    they time out. Flag 4: split 0 tags everything it publishes, and compares what it reads,
+    with a tag no launch has — the other splits never see its maxima or the seeds it selects
+    (their waits on them run to the limit: the first event of every query block times out),
+    and split 0 never sees theirs (it runs unseeded). Results: bitwise the tile kernel's, over
+    several launches, and the launch takes longer by at least one timed-out wait."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(97 + d + B)
+    C = _clustered(rng, n, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, n, dtype="bf16", device=cuda)
+    ix.upsert(C)
+    ref = _run(ix, Q, k, TILELANE, "tilelane128")
+    for flags in (QRES | MUTE, QRES, QRES | MUTE, QRES | MUTE):
+        s, r = _run(ix, Q, k, flags, "qres256")
+        np.testing.assert_array_equal(r, ref[1])
+        np.testing.assert_array_equal(s, ref[0])
+
+    def kernel_ms(flags, reps=20):
+        ix.set_debug_flags(flags)
+        ix.query(Q, k)
+        torch.cuda.synchronize()
+        ix.profile_begin(reps)
+        for _ in range(reps):
+            ix.query(Q, k)
+        torch.cuda.synchronize()
+        prof = ix.profile_end()
+        ix.set_debug_flags(0)
+        return prof["ms_sum"]["tile_topk"] / max(1, prof["calls"])
+
+    plain, muted = kernel_ms(QRES), kernel_ms(QRES | MUTE)
+    ix.close()
+    print(f"seed-wait timeouts d={d} n={n} B={B}: kernel {plain * 1e3:.1f} us, with split 0 muted {muted * 1e3:.1f} us")
+    assert muted > plain + 0.005  # at least one 10-us wait ran out (and split 0 ran unseeded)
+
+
+def test_qres_large_corpus_plan(cuda):
+    """From 512k rows (the corpus streams from HBM) qres256 is planned only where it seeds itself
+    (>= 32 splits: B <= 2048 at k <= 12); larger batches keep kb256."""
+    from ah_rag.embeddings import DenseIndex
+    ix = DenseIndex(768, 600000, dtype="f16", device=cuda)
+    ix.upsert(np.zeros((600000, 768), np.float32))
+    assert ix.plan(1024, 10)["kernel"] == "qres256"
+    assert ix.plan(2048, 10)["kernel"] == "qres256"
+    assert ix.plan(4096, 10)["kernel"] == "kb256"
+    assert ix.plan(8192, 10)["kernel"] == "kb256"
+    ix.set_debug_flags(QRES)
+    assert ix.plan(4096, 10)["kernel"] == "qres256"  # forced
     ix.close()

@@ -11,7 +11,8 @@ the vector store (no encoder weights offline), then times
 Replicas per GPU: --gpus N runs one process per GPU (spawned by this script, or
 under torch.distributed.run), the graph and corpus replicated, the --envs environments
 partitioned over the ranks; no collective on the data path (the job time is the slowest rank's).
-Prints one JSON line. Usage: python tools/bench_env.py [--gpus 8] [--envs 1024] [--steps 6]
+Prints one JSON line. Usage: python tools/bench_env.py [--gpus 8] [--envs 1024] [--steps 6] [--episodes 5]
+[--cpu-seconds 10]
 """
 import argparse
 import json
@@ -38,11 +39,14 @@ def random_actions(rng, masks):
 
 
 def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: int = 1, total_envs=None,
-            backend: str = "nccl") -> dict:
-    """One rank's C5 measurement: build the graph, then a batched VecAHRAGGymEnv episode of `envs`
-    environments (reset + `steps` steps of random valid actions) and, on rank 0, `single`
-    environments stepped one by one. Returns the result dict (the job time is the slowest rank's
-    when world > 1: an all-reduce of the episode time, the only collective)."""
+            backend: str = "nccl", episodes: int = 5, cpu_baseline_fn=None) -> dict:
+    """One rank's C5 measurement: build the graph, then a warm-up episode and `episodes` timed
+    batched VecAHRAGGymEnv episodes of `envs` environments (reset + `steps` steps of random valid
+    actions), with the device time of every search / expansion pass (HIP events, ah_rag.devtime)
+    beside the wall time; on rank 0, `single` environments stepped one by one and, with
+    cpu_seconds > 0, the host restatement of the reference loop (cpu_env_baseline). The job time is
+    the slowest rank's when world > 1 (an all-reduce of the timed episodes, the only collective)."""
+    from ah_rag import devtime
     total_envs = envs if total_envs is None else total_envs
     rng = np.random.default_rng(20251003 + rank)
     t0 = time.perf_counter()
@@ -67,23 +71,36 @@ def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: 
     for _ in range(steps):
         venv.step(random_actions(rng, [e.get_action_mask() for e in venv.envs]))
     barrier()
-    t1 = time.perf_counter()
-    venv.reset(queries, query_vectors=qv)
-    t_reset = time.perf_counter() - t1
-    step_times = []
-    for _ in range(steps):
-        masks = [e.get_action_mask() for e in venv.envs]
-        acts = random_actions(rng, masks)
-        ts = time.perf_counter()
-        venv.step(acts)
-        step_times.append(time.perf_counter() - ts)
-    barrier()
-    vec_time = time.perf_counter() - t1
+    ep_times, reset_wall, step_wall = [], [], [[] for _ in range(steps)]
+    spans = {"reset": [], "step": []}  # (first, last) span index per phase
+    with devtime.recording() as pairs:
+        t1 = time.perf_counter()
+        for _ in range(episodes):
+            te = time.perf_counter()
+            n0 = len(pairs)
+            venv.reset(queries, query_vectors=qv)
+            reset_wall.append(time.perf_counter() - te)
+            spans["reset"].append((n0, len(pairs)))
+            for j in range(steps):
+                masks = [e.get_action_mask() for e in venv.envs]
+                acts = random_actions(rng, masks)
+                ts = time.perf_counter()
+                n0 = len(pairs)
+                venv.step(acts)
+                step_wall[j].append(time.perf_counter() - ts)
+                spans["step"].append((n0, len(pairs)))
+            ep_times.append(time.perf_counter() - te)
+        barrier()
+        vec_time = time.perf_counter() - t1
+        dev_ms = {ph: [devtime.total_ms(pairs[a:b]) for a, b in v] for ph, v in spans.items()}
     if world > 1:  # job time = the slowest rank
         t = torch.tensor([vec_time], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         vec_time = float(t.item())
-    vec_steps = total_envs * (1 + steps)  # all ranks' environments
+    vec_steps = episodes * total_envs * (1 + steps)  # all ranks' environments
+    # (the masks and action draws between steps are the caller's policy, outside the step walls)
+    reset_ms, step_ms = np.mean(reset_wall) * 1e3, float(np.sum([np.mean(w) for w in step_wall])) * 1e3 / steps
+    dev_reset, dev_step = float(np.mean(dev_ms["reset"])), float(np.mean(dev_ms["step"]))
 
     single_rate = None
     if rank == 0 and single > 0:
@@ -101,14 +118,28 @@ def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: 
             for _ in range(steps):
                 env.step(random_actions(rng, [env.get_action_mask()])[0])
         single_rate = round(n1 * (1 + steps) / (time.perf_counter() - ts), 1)
+    cpu = None
+    if rank == 0 and cpu_baseline_fn is not None:
+        cpu = cpu_baseline_fn(hg, ids, vectors, qv, steps)
     return {
         "metric": f"env steps/sec (reset + steps, 2-hop expand + rerank), C5 on {world} MI355X",
         "n_gpus": world, "envs": total_envs, "envs_per_gpu": envs, "steps_per_episode": steps,
+        "episodes": episodes,
         "vec_env_steps_per_s": round(vec_steps / vec_time, 1),
-        "episode_s": round(vec_time, 4),
-        "vec_step_only_per_s_rank0": round(envs * steps / sum(step_times), 1),
-        "vec_reset_ms_rank0": round(t_reset * 1e3, 2), "vec_step_ms_rank0": [round(t * 1e3, 2) for t in step_times],
+        "episode_s": round(vec_time / episodes, 4),
+        "episodes_s": [round(t, 4) for t in ep_times],
+        "vec_step_only_per_s_rank0": round(envs / (step_ms * 1e-3), 1),
+        "vec_reset_ms_rank0": round(reset_ms, 2),
+        "vec_step_ms_rank0": [round(float(np.mean(w)) * 1e3, 2) for w in step_wall],
+        "device_host_split_rank0": {
+            "reset_wall_ms": round(reset_ms, 3), "reset_device_ms": round(dev_reset, 3),
+            "reset_host_ms": round(reset_ms - dev_reset, 3),
+            "step_wall_ms": round(step_ms, 3), "step_device_ms": round(dev_step, 3),
+            "step_host_ms": round(step_ms - dev_step, 3),
+            "how": "device = HIP-event spans around every search / expansion pass (ah_rag.devtime) on the "
+                   "launch stream, summed; host = wall - device; means over the timed episodes"},
         "single_env_steps_per_s": single_rate,
+        "cpu_baseline": cpu,
         "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
         "build_s": round(t_build, 1), "parallelism": f"replicas{world} (environments partitioned, no collective)",
         "data": "synthetic HotpotQA-distractor-shaped graph (SURVEY §8d), seeded corpus vectors, random valid actions",
@@ -128,7 +159,11 @@ def run(a) -> None:
         else:
             dist.init_process_group("gloo")
     envs = a.envs // world + (1 if rank < a.envs % world else 0)  # environments partitioned over ranks
-    out = measure(dev, envs, a.steps, a.single, rank, world, a.envs, a.backend)
+    cpu_fn = None
+    if a.cpu_seconds > 0:
+        from bench import cpu_env_baseline
+        cpu_fn = lambda *x: cpu_env_baseline(*x, budget_s=a.cpu_seconds)  # noqa: E731
+    out = measure(dev, envs, a.steps, a.single, rank, world, a.envs, a.backend, a.episodes, cpu_fn)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -142,6 +177,8 @@ def main():
     ap.add_argument("--envs", type=int, default=1024, help="environments of the whole job")
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--single", type=int, default=32, help="environments stepped one by one (rank 0)")
+    ap.add_argument("--episodes", type=int, default=5, help="timed episodes after the warm-up one")
+    ap.add_argument("--cpu-seconds", type=float, default=0.0, help="host baseline budget (rank 0; 0 = off): bench.cpu_env_baseline")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")
     a = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
