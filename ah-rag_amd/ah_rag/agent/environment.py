@@ -118,13 +118,19 @@ class GraphEnvironment:
         return b
 
     def _observation(self, seeds: List[Dict[str, Any]], reranked: List[Dict[str, Any]]) -> Dict[str, Any]:
+        return self._observation_of(seeds, reranked, self.selection_set, self.frontier_set, self.step_count)
+
+    def _observation_of(self, seeds: List[Dict[str, Any]], reranked: List[Dict[str, Any]], selection_set,
+                        frontier_set, step: int) -> Dict[str, Any]:
+        """The observation dict (reference :118-150) for the given state; VecAHRAGGymEnv builds its
+        environments' observations through this from their state snapshots."""
         obs: Dict[str, Any] = {
             "selection": [self._brief_scored(x) for x in reranked],
             "seeds": [self._brief_scored(x) for x in seeds],
-            "state": {"selection_ids": sorted(self.selection_set),
-                      "frontier_ids": sorted(self.frontier_set)[:50]},
+            "state": {"selection_ids": sorted(selection_set),
+                      "frontier_ids": sorted(frontier_set)[:50]},
             "counts": self._counts(),
-            "step": self.step_count,
+            "step": step,
         }
         if self.debug:
             obs["diagnostics"] = {"filters": self.current_filters, "weights": self.current_weights,
@@ -132,8 +138,9 @@ class GraphEnvironment:
                                   "selection_size": len(self.selection_set)}
         return obs
 
-    def _bare_observation(self, selection: List[Dict[str, Any]]) -> Dict[str, Any]:
-        return {"selection": selection, "seeds": [], "counts": self._counts(), "step": self.step_count}
+    def _bare_observation(self, selection: List[Dict[str, Any]], step: Optional[int] = None) -> Dict[str, Any]:
+        return {"selection": selection, "seeds": [], "counts": self._counts(),
+                "step": self.step_count if step is None else step}
 
     # ---- core API ----------------------------------------------------------------------------
     def reset(self, seed_query: Optional[str] = None, top_k: int = 5) -> Tuple[Dict[str, Any], Dict[str, Any]]:
@@ -232,15 +239,18 @@ class GraphEnvironment:
         self.step_count += 1
         if node_id not in self.hg.G:
             return self._bare_observation([]), {"error": "node_not_found", "node_id": node_id}
-        d = self.hg.G.nodes[node_id]
-        details = {**self._node_brief(node_id), "title": d.get("title"), "name": d.get("name"),
-                   "summary_text": (d.get("summary_text") or d.get("summary") or "")[:500],
-                   "description": (d.get("description") or "")[:500],
-                   "top_words": d.get("top_words"), "members": d.get("members")}
         info = {"action": "query_node_details", "node_id": node_id}
         self._log(info)
         self._record(info)
-        return self._bare_observation([details]), info
+        return self._bare_observation([self._details(node_id)]), info
+
+    def _details(self, node_id: str) -> Dict[str, Any]:
+        """query_node_details' entry for a graph node (reference :301-325)."""
+        d = self.hg.G.nodes[node_id]
+        return {**self._node_brief(node_id), "title": d.get("title"), "name": d.get("name"),
+                "summary_text": (d.get("summary_text") or d.get("summary") or "")[:500],
+                "description": (d.get("description") or "")[:500],
+                "top_words": d.get("top_words"), "members": d.get("members")}
 
     # ---- state & dynamic params --------------------------------------------------------------
     def commit_selection(self, node_ids: List[str]) -> Tuple[Dict[str, Any], Dict[str, Any]]:

@@ -671,6 +671,21 @@ class HierarchicalGraph:
                      return_cluster: bool = False, db_path: Optional[str] = None,
                      model_name: Optional[str] = None, query_vectors: Optional[np.ndarray] = None) -> List[Any]:
         """search() over many queries with one device pass (B = len(queries))."""
+        engine, params, rows, scores, res = self.search_arrays(
+            queries, top_k, member_top_m, alpha, beta, gamma, delta, judge_overall_min, confidence_min, type_filter,
+            db_path, model_name, query_vectors)
+        return [self._assemble(engine, rows[b], scores[b], res, b, params.top_k, return_cluster)
+                for b in range(rows.shape[0])]
+
+    def search_arrays(self, queries: Sequence[str], top_k: int = 5, member_top_m: int = 5,
+                      alpha: Optional[float] = None, beta: Optional[float] = None, gamma: Optional[float] = None,
+                      delta: Optional[float] = None, judge_overall_min: Optional[float] = None,
+                      confidence_min: Optional[float] = None, type_filter: Optional[List[str]] = None,
+                      db_path: Optional[str] = None, model_name: Optional[str] = None,
+                      query_vectors: Optional[np.ndarray] = None):
+        """search_batch() before the result dicts: (engine, params, dense rows [B,k], dense scores
+        [B,k], host RerankResult); _assemble(engine, rows[b], scores[b], res, b, ...) turns query b
+        into search()'s return value. VecAHRAGGymEnv works on these arrays directly."""
         params = resolve_search_params(self.G.graph.get("search_params", {}), top_k, member_top_m, alpha, beta,
                                        gamma, delta, judge_overall_min, confidence_min, type_filter)
         vi = self.G.graph.get("vector_index") if isinstance(self.G.graph.get("vector_index"), dict) else {}
@@ -693,8 +708,7 @@ class HierarchicalGraph:
         if q.dim() == 1:
             q = q.unsqueeze(0)
         rows, scores, res = engine.run(q, params)
-        return [self._assemble(engine, rows[b], scores[b], res, b, params.top_k, return_cluster)
-                for b in range(q.shape[0])]
+        return engine, params, rows, scores, res
 
     def _assemble(self, engine: SearchEngine, rows, scores, res, b: int, top_k: int, return_cluster: bool):
         seeds = []

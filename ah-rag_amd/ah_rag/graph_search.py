@@ -323,7 +323,8 @@ class SearchEngine:
         self.graph = graph
         n = graph.n_nodes
         rows = np.asarray([graph.index.get(r, n + i) for i, r in enumerate(self.row_ids)], np.int32)
-        self.row_to_node = torch.from_numpy(rows if len(rows) else np.zeros(1, np.int32)).to(graph.device)
+        self.row_to_node_host = rows if len(rows) else np.zeros(1, np.int32)
+        self.row_to_node = torch.from_numpy(self.row_to_node_host).to(graph.device)
 
     def node_id(self, idx: int) -> str:
         n = self.graph.n_nodes

@@ -38,6 +38,27 @@ def random_actions(rng, masks):
     return [int(rng.choice(np.flatnonzero(np.asarray(m)))) for m in masks]
 
 
+def random_actions_batch(rng, masks: np.ndarray) -> np.ndarray:
+    """A uniformly random valid action per row of an [E, 6] mask (the batched policy's draw)."""
+    u = rng.random(masks.shape) * (masks > 0)
+    return np.argmax(u, axis=1)
+
+
+def single_reset(env: AHRAGGymEnv, hg, query: str, qvec: np.ndarray):
+    """AHRAGGymEnv.reset(query) with a precomputed query vector (no encoder weights offline): the
+    same GraphEnvironment.reset + semantic_anchor steps (environment.py:155-241), the search at B = 1."""
+    ge = env.env
+    env._query, env._cur_step = query, 0
+    ge.last_query, ge.last_results, ge.step_count = None, None, 0
+    ge.selection_set.clear()
+    ge.frontier_set.clear()
+    ge.step_count += 1
+    ge.last_query = query
+    cluster = hg.search_batch([query], top_k=5, member_top_m=5, return_cluster=True, query_vectors=qvec)[0]
+    obs, _ = ge._anchor_result(query, 5, cluster, 0.0)
+    return env._finish_reset(obs)
+
+
 def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: int = 1, total_envs=None,
             backend: str = "nccl", episodes: int = 5, cpu_baseline_fn=None) -> dict:
     """One rank's C5 measurement: build the graph, then a warm-up episode and `episodes` timed
@@ -69,7 +90,7 @@ def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: 
     # warm-up episode: device graph, index, expansion kernels, host caches
     venv.reset(queries, query_vectors=qv)
     for _ in range(steps):
-        venv.step(random_actions(rng, [e.get_action_mask() for e in venv.envs]))
+        venv.step(random_actions_batch(rng, venv.action_masks()))
     barrier()
     ep_times, reset_wall, step_wall = [], [], [[] for _ in range(steps)]
     spans = {"reset": [], "step": []}  # (first, last) span index per phase
@@ -82,8 +103,7 @@ def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: 
             reset_wall.append(time.perf_counter() - te)
             spans["reset"].append((n0, len(pairs)))
             for j in range(steps):
-                masks = [e.get_action_mask() for e in venv.envs]
-                acts = random_actions(rng, masks)
+                acts = random_actions_batch(rng, venv.action_masks())  # the policy's batched draw
                 ts = time.perf_counter()
                 n0 = len(pairs)
                 venv.step(acts)
@@ -111,10 +131,8 @@ def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: 
         hg.search_batch(queries[:1], top_k=5, return_cluster=True, query_vectors=qv[:1])
         ts = time.perf_counter()
         for i in range(n1):
-            # reset with a precomputed vector: the same path VecAHRAGGymEnv uses, at B = 1
-            sub = VecAHRAGGymEnv.__new__(VecAHRAGGymEnv)
-            sub.hg, sub.envs = hg, [env]
-            sub.reset([queries[i]], query_vectors=qv[i:i + 1])
+            # reset with a precomputed vector (the search at B = 1)
+            single_reset(env, hg, queries[i], qv[i:i + 1])
             for _ in range(steps):
                 env.step(random_actions(rng, [env.get_action_mask()])[0])
         single_rate = round(n1 * (1 + steps) / (time.perf_counter() - ts), 1)
