@@ -1997,8 +1997,15 @@ __global__ __launch_bounds__(64) void merge_lane_lists_kernel(const uint64_t* __
   const int lane = threadIdx.x;
   const uint64_t* src = in + ((int64_t)q * n_lists + lane) * k_in;
   uint64_t L[KCAP];
+  // a list ends at its first empty slot (key 0): the register-resident kernel writes only its kept
+  // keys and one terminating 0 (kFlagShortLists), so the slots after it hold another launch's keys
+  bool end = false;
 #pragma unroll
-  for (int j = 0; j < KCAP; ++j) L[j] = (lane < n_lists && j < k_in) ? src[j] : 0;
+  for (int j = 0; j < KCAP; ++j) {
+    const uint64_t v = (lane < n_lists && j < k_in) ? src[j] : 0;
+    end = end || v == 0;
+    L[j] = end ? 0 : v;
+  }
   // lane j keeps output j (k <= 64): one coalesced store per output array at the end instead of a
   // lane-0 store per round
   uint64_t mine = 0;
@@ -3332,8 +3339,13 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.qblocks = 1;
     const bool f32 = ix->dtype == AHR_F32;  // 64-row items (a row per lane) vs 16-row blocks
     p.n_row_tiles = (int)cdiv(ix->count, f32 ? 64 : 16);
+    // AHR_SMALL_SPLITS (A/B): workgroups per launch, up to 512 (two per CU co-reside: <= 128 VGPRs)
+    static const int split_env = [] {
+      const char* e = getenv("AHR_SMALL_SPLITS");
+      return e ? std::max(1, std::min(512, atoi(e))) : 256;
+    }();
     p.n_splits = (int)std::max<int64_t>(
-        1, std::min<int64_t>(256, cdiv(p.n_row_tiles, f32 ? smallf32::kWaves : small::waves(1))));
+        1, std::min<int64_t>(split_env, cdiv(p.n_row_tiles, f32 ? smallf32::kWaves : small::waves(1))));
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     p.xcd_remap = false;
     return p;
@@ -3680,8 +3692,10 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       // [256 qblocks][n_splits] maxima and [256 qblocks] seeds
       const QresSchedule sch = qres_schedule();
       const bool once = (flags & kFlagQresSeedOnce) != 0;
+      // (<= 64 splits: the lane-list merge follows, which stops at a list's first empty slot)
+      const uint32_t qflags = flags | (p.n_splits <= 64 ? kFlagShortLists : 0u);
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
-                   p.n_splits, p.qblocks, (int)flags, self_seed ? ix->ss + kQresTagOff + 1 : nullptr, once ? 1 : sch.pub,
+                   p.n_splits, p.qblocks, (int)qflags, self_seed ? ix->ss + kQresTagOff + 1 : nullptr, once ? 1 : sch.pub,
                    once ? 0 : sch.ev, s);
       return;
     }

@@ -242,6 +242,9 @@ enum : uint32_t {
   kFlagQresTrace = 1u << 29,  // qres kernel: per-workgroup timestamps into AHR_QRES_TRACE_PTR (ablation build)
   kFlagQresEvNoSel = 1u << 30,   // qres seeding events without the selection (wrong seeds: ablation build)
   kFlagQresEvNoIssue = 1u << 31, // qres seeding events without the landing reads (ablation build)
+  // internal (set by the library on a launch, never accepted from a caller): the qres kernel ends
+  // each (query, split) list at its first empty slot, for the lane-list merge, which stops there
+  kFlagShortLists = 65536,
 };
 #ifdef AHR_ABLATION
 constexpr bool kAblation = true;  // the profiling build: cost-split switches compiled in

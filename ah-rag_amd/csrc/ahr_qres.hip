@@ -52,6 +52,7 @@ namespace qres {
 // (48 or 24 KiB). 24-KiB stages run a 3-slot ring issued two blocks ahead, 48-KiB stages a 2-slot
 // ring issued one block ahead.
 constexpr int kLandBytes = 768;
+
 static_assert(kPark >= 6, "the replay of a parked block never overtakes its unread quads");
 
 template <int NKT>
@@ -358,7 +359,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       }
     }
   };
-  float rm = -INFINITY;  // self-seeding: max score of this lane's rows so far
+  // self-seeding: max score of this lane's rows so far, as its ordered bits with bit 0 set while it
+  // has risen since the last publication (ord(-inf) is odd: the first publication always writes)
+  uint32_t rmo = ord_f32(-INFINITY) | 1u;
   // a block's 16 scores of this lane: quad maxima, then the passing quads
   auto screen_quads = [&](const f32x16& acc, int r0) __attribute__((always_inline)) {
     float qm[4];
@@ -368,13 +371,14 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const float m = fmaxf(fmaxf(qm[0], qm[1]), fmaxf(qm[2], qm[3]));
     const bool ragged = r0 + kTR > n_rows;  // wave-uniform: the last block only
     if (ss) {
-      if (!ragged) {
-        rm = fmaxf(rm, m);
-      } else {
+      float bm = m;
+      if (ragged) {
+        bm = -INFINITY;
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-          if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) rm = fmaxf(rm, acc[j]);
+          if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) bm = fmaxf(bm, acc[j]);
       }
+      rmo = max(rmo, ord_f32(bm) | 1u);  // a new maximum is marked risen
     }
     if (m < thr) return;
 #pragma unroll
@@ -393,11 +397,24 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // cross-XCD read never holds up the ring. Each counted site issues exactly one instruction per
   // wave (some lane is always active there).
   int young = 0;
+  // (the per-lane event table, built below: see event_site)
+  uint32_t* const tab = reinterpret_cast<uint32_t*>(smem + C::kOffTab) + wave * 64;
+  // A publication writes only the maxima that rose since the split's previous one (the others'
+  // granules still hold this launch's current values): one buffer store per wave whatever the
+  // lanes' state — a lane with nothing to write gets an out-of-range offset, which the buffer
+  // unit drops — so the count of younger operations stays exact (round 5: WRITE per C2 launch
+  // 29.7 MB -> see DESIGN §3.0). The published value is the maximum with bit 0 cleared, at most
+  // one ulp below it: still a lower bound.
   auto publish = [&]() __attribute__((always_inline)) {
-    const float pm = fmaxf(rm, __shfl_xor(rm, 32, 64));  // the query's max over this split's rows
+    const uint32_t pm = max(rmo, (uint32_t)__shfl_xor((int)rmo, 32, 64));  // the query's max over this split's rows
     int qq = q;
     asm volatile("" : "+v"(qq));
-    if (!fh && qq < n_q) granule_store(pub + (int64_t)qq * n_splits + split, ((uint64_t)epoch << 32) | ord_f32(pm));
+    const uint32_t off = !fh && qq < n_q && (pm & 1u) ? (uint32_t)(qq * n_splits + split) * 8u : 0xFFFFFFF0u;
+    const u32x4 uni = *reinterpret_cast<const u32x4*>(tab + 48);  // (the buffer size: see the event table)
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(pub, (uint32_t)__builtin_amdgcn_readfirstlane((int)uni[2]));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{pm & ~1u, epoch}, r, (int)off, 0, 16);  // sc1: write-through
+    rmo &= ~1u;
     ++young;
   };
   auto apply_seed = [&](uint64_t g) __attribute__((always_inline)) {  // a seed granule of this launch raises thr
@@ -424,7 +441,6 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // the byte offset in the self-seeding buffer); lanes 48..52 the wave's count of selected queries,
   // the first one's index in the query block, the buffer's byte size, the offset of the wave's
   // seeds and the index step between its selected queries.
-  uint32_t* const tab = reinterpret_cast<uint32_t*>(smem + C::kOffTab) + wave * 64;
   if (ss) {
     const int ns = n_splits;
     const int np = ns >= 128 ? 32 : ns / 2;  // lanes per selected query
@@ -608,9 +624,11 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     const int r0 = (b_begin + bi) * kTR;
     if (ss && bi == 0) {  // the first event's sample: park the scores, publish the maxima
       park(acc);
+      float bm = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 16; ++j)  // block 0 is never ragged (>= 2 blocks per split) but check anyway
-        if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) rm = fmaxf(rm, acc[j]);
+        if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) bm = fmaxf(bm, acc[j]);
+      rmo = max(rmo, ord_f32(bm) | 1u);
       publish();
       return;
     }
@@ -709,9 +727,13 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       list_insert<kListCap>(L, v);
     }
     uint64_t* dst = part_keys + ((int64_t)q * n_splits + split) * k_out;
+    // kFlagShortLists (the merge that follows stops at a list's first empty slot): the kept keys
+    // and one terminating 0, not the whole k slots (most (query, split) lists hold 0-2 keys above
+    // the final threshold)
+    const bool short_lists = (flags & kFlagShortLists) != 0;
 #pragma unroll
     for (int j = 0; j < kListCap; ++j)
-      if (j < k_out) dst[j] = L[j];
+      if (j < k_out && (!short_lists || j == 0 || L[j - 1] != 0)) dst[j] = L[j];
   }
   if (bal && tid == 0)
     __hip_atomic_fetch_add(xcdw + 8 + (split & 7), (uint32_t)__builtin_amdgcn_s_memrealtime() - tab[60],
@@ -752,7 +774,7 @@ void launch_t(const uint8_t* rows, const uint8_t* qfrag, int64_t row_stride, int
     switch (abl) {
       AHR_QRES_ABL(1) AHR_QRES_ABL(3) AHR_QRES_ABL(5) AHR_QRES_ABL(13) AHR_QRES_ABL(17) AHR_QRES_ABL(31)
       AHR_QRES_ABL(32) AHR_QRES_ABL(64) AHR_QRES_ABL(128) AHR_QRES_ABL(192) AHR_QRES_ABL(96) AHR_QRES_ABL(160)
-      AHR_QRES_ABL(224)
+      AHR_QRES_ABL(224) AHR_QRES_ABL(2) AHR_QRES_ABL(8) AHR_QRES_ABL(16) AHR_QRES_ABL(12)
       default: break;
     }
 #undef AHR_QRES_ABL

@@ -353,15 +353,20 @@ def time_queries(ix, q, k: int, steps: int, warmup: int, inflight: int, dev):
     return dt, ix.profile_end(), res
 
 
-def cold_kernel_ms(ix, q, k: int, reps: int, dev) -> float:
+def cold_kernel_ms(ix, q, k: int, reps: int, dev, dirty: bool = False) -> float:
     """Average event-timed tile-kernel time of `ix.query(q, k)` with L2 and the Infinity Cache
-    flushed before every query (a 512 MiB write on the same stream, outside the kernel's events)."""
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    flushed before every query, outside the kernel's events: by a 512 MiB read (the caches then
+    hold clean lines of another buffer), or with dirty=True by a 512 MiB write (the query's reads
+    then also pay the write-back of up to 256 MiB of dirty lines — not the kernel's traffic)."""
+    flush = torch.zeros(128 << 20, dtype=torch.float32, device=dev)
     ix.query(q, k)
     torch.cuda.synchronize()
     ix.profile_begin(reps)
     for _ in range(reps):
-        flush.fill_(1)
+        if dirty:
+            flush.fill_(1.0)
+        else:
+            flush.amax()
         ix.query(q, k)
     torch.cuda.synchronize()
     prof = ix.profile_end()
@@ -732,6 +737,23 @@ def run(args) -> None:
                 "roofline": {"bound": "mfma", "achieved": round(f_tf, 2), "peak": MFMA_PEAK_TFLOPS["f32"],
                              "unit": "TFLOP/s", "frac": round(f_tf / MFMA_PEAK_TFLOPS["f32"], 4)},
             }
+            if not args.no_batch_sweep:
+                # B = 1 on the fp32 index: the drop-in search() / GraphEnvironment default
+                # (hierarchical_graph.py:712-714 per env reset), the exact-mode streaming kernel
+                q1 = q[:1].contiguous()
+                b_steps = args.steps * 4
+                b_dt, b_prof, _ = time_queries(f32, q1, k, b_steps, args.warmup, args.inflight or auto_inflight(f32, 1, k), dev)
+                b_calls = max(1, b_prof["calls"])
+                b_plan = f32.plan(1, k)
+                e1 = {"batch": 1, "value": round(b_steps / b_dt, 1), "unit": "queries/s",
+                      "ms_per_step": round(b_dt / b_steps * 1e3, 4), "steps": b_steps, "launch": b_plan,
+                      "stages_ms_per_step": {kk: round(v / b_calls, 4) for kk, v in b_prof["ms_sum"].items()},
+                      "roofline": roofline(b_plan, "f32", 1, N, d, k, b_prof["ms_sum"]["tile_topk"] / b_calls, workload)}
+                e1["roofline"]["note"] = "corpus Infinity-Cache resident between queries (warm)"
+                cold_ms = cold_kernel_ms(f32, q1, k, max(10, args.steps), dev)
+                e1["roofline_cold_caches"] = roofline(b_plan, "f32", 1, N, d, k, cold_ms, workload)
+                e1["roofline_cold_caches"]["note"] = "L2 and Infinity Cache refilled with clean lines before each query"
+                out["exact_fp32"]["batch1"] = e1
             f32.close()
         if world == 1 and workload == "hotpot90k" and not args.no_batch_sweep:
             # BASELINE.md's C2 batch sweep beside the B = 1024 headline: B = 1 (the drop-in
@@ -757,7 +779,10 @@ def run(args) -> None:
                     entry["roofline"]["note"] = "corpus Infinity-Cache resident between queries (warm)"
                     cold_ms = cold_kernel_ms(local, qb, k, max(10, args.steps), dev)
                     entry["roofline_cold_caches"] = roofline(b_plan, dtype, b, N, d, k, cold_ms, workload)
-                    entry["roofline_cold_caches"]["note"] = "L2 and Infinity Cache flushed before each query"
+                    entry["roofline_cold_caches"]["note"] = ("L2 and Infinity Cache refilled with clean lines (a 512 MiB "
+                                                             "read) before each query")
+                    entry["roofline_cold_caches"]["avg_launch_ms_dirty_caches"] = round(
+                        cold_kernel_ms(local, qb, k, max(10, args.steps), dev, dirty=True), 5)
                 out["batch_sweep"].append(entry)
         if world == 1 and workload == "hotpot90k" and not args.no_sublines:
             # configs[2] and configs[4] under the driver's clock, beside the configs[1] headline

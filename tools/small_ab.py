@@ -20,13 +20,16 @@ from ah_rag.embeddings import DenseIndex  # noqa: E402
 from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus  # noqa: E402
 
 
-def stage_ms(ix, q, k, reps, flush=None):
+def stage_ms(ix, q, k, reps, flush=None, mode="read"):
     ix.query(q, k)
     torch.cuda.synchronize()
     ix.profile_begin(reps)
     for _ in range(reps):
         if flush is not None:
-            flush.fill_(1)
+            if mode == "read":
+                flush.amax()
+            else:
+                flush.fill_(1.0)
         ix.query(q, k)
     torch.cuda.synchronize()
     p = ix.profile_end()
@@ -42,7 +45,7 @@ def main():
     corpus = SyntheticCorpus(HOTPOT_90K, dev)
     rows = corpus.rows()
     q, _ = corpus.queries(16, rows)
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    flush = torch.zeros(128 << 20, dtype=torch.float32, device=dev)
     out = {"lib": os.environ.get("AHR_LIB_PATH", "in-tree")}
     for dtype in ("bf16", "f32"):
         ix = DenseIndex(768, rows.shape[0], dtype=dtype, device=dev)
@@ -53,8 +56,9 @@ def main():
             qb = q[:b].contiguous()
             plan = ix.plan(b, 10)["kernel"]
             warm = stage_ms(ix, qb, 10, a.reps)
-            cold = stage_ms(ix, qb, 10, a.reps, flush)
-            out[f"{dtype}_b{b}"] = {"plan": plan, "warm_us": warm, "cold_us": cold}
+            cold = stage_ms(ix, qb, 10, a.reps, flush, "read")
+            dirty = stage_ms(ix, qb, 10, a.reps, flush, "write")
+            out[f"{dtype}_b{b}"] = {"plan": plan, "warm_us": warm, "cold_us": cold, "cold_dirty_us": dirty}
         ix.close()
     print(json.dumps(out), flush=True)
 
