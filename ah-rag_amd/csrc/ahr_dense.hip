@@ -2339,6 +2339,43 @@ __global__ __launch_bounds__(256) void convert_queries_frag_kernel(const float* 
   convert_row_fast(src + i * dim, dim, normalize, dst + i * row_stride, d_pad, dt, lane, frag, i);
 }
 
+// The register-resident plan's fragment-major query copy straight from the fp32 queries, when
+// nothing else reads the row-major copy (self-seeded launches: no pre-pass) and the rows need no
+// normalisation: one thread per 16-B chunk of the copy (query 32 g + l % 32, dims 16 S + 8 (l / 32)
+// .. + 8, the convert kernel's rounding), so a wave writes one contiguous KiB. The row-major
+// convert wrote each 16-B chunk as two 8-B pieces 1 KiB apart, plus the unused rows.
+__global__ __launch_bounds__(256) void frag_from_f32_kernel(const float* __restrict__ src, int64_t n, int dim, int d_pad,
+                                                            int dt, int64_t n16, uint8_t* __restrict__ frag,
+                                                            uint32_t* __restrict__ epoch) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i == 0 && epoch) advance_epoch_rebalance(epoch);  // the next qres launch's tag
+  if (i >= n16) return;
+  const int l = (int)(i & 63);
+  const int ns = d_pad >> 4;
+  const int64_t gs = i >> 6;
+  const int S = (int)(gs % ns);
+  const int64_t q = (gs / ns) * 32 + (l & 31);
+  const int j0 = 16 * S + 8 * (l >> 5);
+  float v[8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x4 w = {0.f, 0.f, 0.f, 0.f};
+    if (q < n && j0 + 4 * h < dim) w = *reinterpret_cast<const f32x4*>(src + q * dim + j0 + 4 * h);  // dim % 4 == 0
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * h + e] = w[e];
+  }
+  u32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (dt == DT_BF16)
+      o[e] = (uint32_t)f32_to_bf16_rne(v[2 * e]) | ((uint32_t)f32_to_bf16_rne(v[2 * e + 1]) << 16);
+    else
+      o[e] = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[2 * e]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[2 * e + 1]) << 16);
+  }
+  *reinterpret_cast<u32x4*>(frag + i * 16) = o;
+}
+
 // fp32 rows -> storage rows (one wave per row): optional L2 normalisation, dtype conversion,
 // zero padding to d_pad, fp32 lane permutation. Lanes move 4 consecutive elements at a time.
 __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restrict__ src, int64_t n,
@@ -2723,9 +2760,23 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
 namespace smallf32 {
 constexpr int kWaves = 8;
 constexpr int kMaxQ = 4;
+// A/B knobs: AHR_F32_LPS = 128-B lines per step at B = 1 (1 or 2; 2 needs an even line count),
+// AHR_F32_WPS = busy waves per workgroup the split count aims at (8: ceil(items / 8) workgroups)
+inline int env_int(const char* name, int dflt, int lo, int hi) {
+  const char* e = getenv(name);
+  return e ? std::max(lo, std::min(hi, atoi(e))) : dflt;
+}
+inline int lines_per_step(int n_lines) {
+  static const int lps = env_int("AHR_F32_LPS", 1, 1, 2);
+  return lps == 2 && n_lines % 2 == 0 ? 2 : 1;
+}
+inline int waves_per_split() {
+  static const int w = env_int("AHR_F32_WPS", kWaves, 1, kWaves);
+  return w;
+}
 }  // namespace smallf32
 
-template <int KCAP, int NQ>
+template <int KCAP, int NQ, int LPS>
 __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qconv, int64_t row_stride, int n_rows, int n_q,
     int n_lines, int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
@@ -2743,13 +2794,14 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
   const int i_end = (int)((int64_t)(split + 1) * n_items / n_splits);
   const int d_pad = (int)(row_stride >> 2);
 
-  u32x4 A0[8], A1[8];
-  int ci = i_begin + wave, cl = 0;  // current item, current 128-B line of the row
-  auto load_line = [&](u32x4 (&A)[8], int item, int line) __attribute__((always_inline)) {
+  // LPS 128-B lines of the row per step (n_lines % LPS == 0): one register set = LPS lines
+  u32x4 A0[8 * LPS], A1[8 * LPS];
+  int ci = i_begin + wave, cl = 0;  // current item, first 128-B line of the step
+  auto load_line = [&](u32x4 (&A)[8 * LPS], int item, int line) __attribute__((always_inline)) {
     const int row = item * 64 + lane;
     const u32x4* src = reinterpret_cast<const u32x4*>(corpus + (int64_t)row * row_stride + line * 128);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) A[j] = src[j];
+    for (int j = 0; j < 8 * LPS; ++j) A[j] = src[j];
   };
   if (ci < i_end) load_line(A0, ci, 0);
   for (int i = tid; i < n_q * d_pad / 4; i += W * 64) {
@@ -2769,8 +2821,8 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
     thk[q] = 0;
     acc[q] = 0.f;
   }
-  auto step = [&](u32x4 (&C)[8], u32x4 (&N)[8]) __attribute__((always_inline)) {
-    int ni = ci, nl = cl + 1;
+  auto step = [&](u32x4 (&C)[8 * LPS], u32x4 (&N)[8 * LPS]) __attribute__((always_inline)) {
+    int ni = ci, nl = cl + LPS;
     if (nl >= n_lines) {
       nl = 0;
       ni += W;
@@ -2780,7 +2832,7 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
       load_line(N, more ? ni : ci, more ? nl : cl);
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {  // 4 groups of 8 per line
+    for (int g = 0; g < 4 * LPS; ++g) {  // 4 groups of 8 per line
       const f32x4 lo = __builtin_bit_cast(f32x4, C[2 * g]);
       const f32x4 hi = __builtin_bit_cast(f32x4, C[2 * g + 1]);
 #pragma unroll
@@ -3310,6 +3362,13 @@ inline QresSchedule qres_schedule() {
   return sch;
 }
 
+// The register-resident kernel seeds itself (no pre-pass launch) unless kFlagQresPrepass asks for
+// the sampled pre-pass (A/B) or the caller supplies seeds.
+inline bool qres_self_seeded(const ahr_index* ix, const SearchPlan& p, int k) {
+  return p.kernel == KERNEL_QRES && sample_rows_for(ix) > 0 && !ix->seed && !(ix->debug_flags & kFlagQresPrepass) &&
+         qres::self_seeds(ix->count, p.n_splits, k);
+}
+
 // the second query buffer (the register-resident plan's fragment-major copy, or the k-blocked
 // copy of the kb256 plan), zeroed on the caller's stream when allocated
 int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
@@ -3345,7 +3404,7 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
       return e ? std::max(1, std::min(512, atoi(e))) : 256;
     }();
     p.n_splits = (int)std::max<int64_t>(
-        1, std::min<int64_t>(split_env, cdiv(p.n_row_tiles, f32 ? smallf32::kWaves : small::waves(1))));
+        1, std::min<int64_t>(split_env, cdiv(p.n_row_tiles, f32 ? smallf32::waves_per_split() : small::waves(1))));
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     p.xcd_remap = false;
     return p;
@@ -3627,14 +3686,17 @@ void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, 
   float* fs = fold ? fold->scores : nullptr;
   int32_t* fr = fold ? fold->rows : nullptr;
   uint64_t* fk = fold ? fold->keys : nullptr;
-  if (B == 1)
-    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 1>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), lds, s,
-                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part,
-                       fc, fs, fr, fk);
+#define AHR_F32_LAUNCH(NQ, LPS)                                                                                   \
+  hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, NQ, LPS>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), \
+                     lds, s, ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k,  \
+                     ix->part, fc, fs, fr, fk)
+  if (B == 1 && smallf32::lines_per_step(n_lines) == 2)
+    AHR_F32_LAUNCH(1, 2);
+  else if (B == 1)
+    AHR_F32_LAUNCH(1, 1);
   else
-    hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, 4>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), lds, s,
-                       ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part,
-                       fc, fs, fr, fk);
+    AHR_F32_LAUNCH(4, 1);
+#undef AHR_F32_LAUNCH
 }
 
 template <int DT>
@@ -3662,10 +3724,7 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     }
   }
   const int S = sample_rows_for(ix);
-  // the register-resident kernel seeds itself (no pre-pass launch) unless kFlagQresPrepass asks for
-  // the sampled pre-pass (A/B) or the caller supplies seeds
-  const bool self_seed = p.kernel == KERNEL_QRES && S > 0 && !ix->seed && !(ix->debug_flags & kFlagQresPrepass) &&
-                         qres::self_seeds(ix->count, p.n_splits, k);
+  const bool self_seed = qres_self_seeded(ix, p, k);
   if (ix->seed) {
     thr = ix->seed;  // the caller's valid lower bounds of each query's k-th best score
   } else if (!self_seed && S > 0 && ix->count >= 4 * (int64_t)S && k * 16 <= S) {
@@ -3848,7 +3907,13 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
       if (ix->qres_multi) AHR_HIP(hipStreamWaitEvent(s, ix->qres_done, 0));
       ix->qres_multi = true;  // from the next batch on (this one's predecessor recorded nothing)
     }
-    if (small_fuses_convert(ix)) {  // one launch: rows + fragments
+    if (small_fuses_convert(ix) && !normalize_q && qres_self_seeded(ix, plan_search(ix, B, k), k)) {
+      // only the fragment-major copy: the self-seeded launch reads nothing else
+      const int64_t n16 = cdiv(B, 32) * (ix->d_pad / 16) * 64;
+      hipLaunchKernelGGL(frag_from_f32_kernel, dim3((unsigned)cdiv(n16, 256)), dim3(256), 0, s, q, (int64_t)B, ix->dim,
+                         ix->d_pad, ix->dtype, n16, ix->qbuf_kb, reinterpret_cast<uint32_t*>(ix->ss + kQresTagOff));
+      frag_done = true;
+    } else if (small_fuses_convert(ix)) {  // one launch: rows + fragments
       hipLaunchKernelGGL(convert_queries_frag_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q, (int64_t)B,
                          ix->dim, normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, ix->dtype, ix->qbuf_kb,
                          reinterpret_cast<uint32_t*>(ix->ss + kQresTagOff));
