@@ -2751,40 +2751,51 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
 // drop-in search's fp32 index. The exact-mode contract is one fmaf chain per (row, query) in
 // increasing k, so one lane owns one corpus row of a 64-row item and runs the chain on the VALU
 // (B <= 4 queries: <= 4 fmas per loaded float, far below the stream's cost); the stored (evens |
-// odds) permutation of each group of 8 is undone by the order of the fmas. Loads: one 128-B line
-// per lane per step in two register sets (the next step's line in flight under the current
-// fmas). Queries (the convert kernel's permuted fp32 rows) are broadcast reads from LDS. Each
-// lane keeps a register list per query; at the end every wave reduces its 64 lane lists (k rounds
-// of a DPP wave max) and one wave merges the 8 wave lists through LDS into one list per
-// (query, split).
+// odds) permutation of each group of 8 is undone by the order of the fmas. Loads: a step is one
+// 128-B line of the item's 64 rows, brought in by LDS-DMA as whole lines (8 rows per
+// wave-instruction) into a two-slot per-wave ring, the next step's line in flight under the
+// current fmas; each lane then reads its own row's line from the slot (swizzled, conflict-free).
+// The round-1 form (per-lane 16-B register loads: 64 lines per instruction) stays behind
+// AHR_F32_SLOTS=0 for A/B. One workgroup per CU (up to 256 splits; ~5.5 items per split at C2).
+// Queries (the convert kernel's permuted fp32 rows) are broadcast reads from LDS. Each lane keeps
+// a register list per query; at the end every wave reduces its 64 lane lists (k rounds of a DPP
+// wave max) and one wave merges the 8 wave lists through LDS into one list per (query, split).
 namespace smallf32 {
 constexpr int kWaves = 8;
 constexpr int kMaxQ = 4;
-// A/B knobs: AHR_F32_LPS = 128-B lines per step at B = 1 (1 or 2; 2 needs an even line count),
-// AHR_F32_WPS = busy waves per workgroup the split count aims at (8: ceil(items / 8) workgroups)
+// lines of the ring per wave: 0 = per-lane register loads (two register sets), 2 = LDS-DMA slots
+// of one 64-row x 128-B line image each (8 KiB). (3 slots, 6 waves: measured equal to 2 at B = 1;
+// the kernel is written for any depth, only 0 and 2 are built.)
+__host__ __device__ constexpr int waves_for(int slots) { return slots == 3 ? 6 : kWaves; }
+__host__ __device__ constexpr int ring_bytes(int slots) { return slots ? waves_for(slots) * slots * 8192 : 0; }
+// A/B knobs: AHR_F32_SLOTS (0 or 2), AHR_F32_WPS = busy waves per workgroup the split count aims at
+// (1: up to 256 workgroups, one per CU; 8: the round-1 geometry)
 inline int env_int(const char* name, int dflt, int lo, int hi) {
   const char* e = getenv(name);
   return e ? std::max(lo, std::min(hi, atoi(e))) : dflt;
 }
-inline int lines_per_step(int n_lines) {
-  static const int lps = env_int("AHR_F32_LPS", 1, 1, 2);
-  return lps == 2 && n_lines % 2 == 0 ? 2 : 1;
+inline int slots() {
+  static const int v = env_int("AHR_F32_SLOTS", 2, 0, 2);
+  return v == 1 ? 2 : v;
 }
 inline int waves_per_split() {
-  static const int w = env_int("AHR_F32_WPS", kWaves, 1, kWaves);
+  static const int w = env_int("AHR_F32_WPS", 1, 1, kWaves);
   return w;
 }
 }  // namespace smallf32
 
-template <int KCAP, int NQ, int LPS>
-__global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kernel(
+template <int KCAP, int NQ, int SLOTS>
+__global__ __launch_bounds__(smallf32::waves_for(SLOTS) * 64, 1) void topk_small_f32_kernel(
     const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qconv, int64_t row_stride, int n_rows, int n_q,
     int n_lines, int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
     uint32_t* __restrict__ fold_ctr, float* __restrict__ out_s, int32_t* __restrict__ out_r,
     uint64_t* __restrict__ out_keys) {
-  constexpr int W = smallf32::kWaves;
+  constexpr int W = smallf32::waves_for(SLOTS);
+  constexpr bool DMA = SLOTS != 0;
   __shared__ __attribute__((aligned(16))) float qs[NQ * 1024];  // d_pad <= 1024
   __shared__ uint64_t wl[NQ][W][KCAP];
+  // DMA form: the line ring (W waves x SLOTS x 8 KiB), later overlaid by the fold's lists
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -2794,16 +2805,53 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
   const int i_end = (int)((int64_t)(split + 1) * n_items / n_splits);
   const int d_pad = (int)(row_stride >> 2);
 
-  // LPS 128-B lines of the row per step (n_lines % LPS == 0): one register set = LPS lines
-  u32x4 A0[8 * LPS], A1[8 * LPS];
-  int ci = i_begin + wave, cl = 0;  // current item, first 128-B line of the step
-  auto load_line = [&](u32x4 (&A)[8 * LPS], int item, int line) __attribute__((always_inline)) {
+  u32x4 A0[8], A1[8];
+  int ci = i_begin + wave, cl = 0;  // current item, current 128-B line of the row
+  auto load_line = [&](u32x4 (&A)[8], int item, int line) __attribute__((always_inline)) {
     const int row = item * 64 + lane;
     const u32x4* src = reinterpret_cast<const u32x4*>(corpus + (int64_t)row * row_stride + line * 128);
 #pragma unroll
-    for (int j = 0; j < 8 * LPS; ++j) A[j] = src[j];
+    for (int j = 0; j < 8; ++j) A[j] = src[j];
   };
-  if (ci < i_end) load_line(A0, ci, 0);
+  // DMA form: a line of the item's 64 rows comes in as 8 wave-instructions of 8 whole 128-B lines
+  // each (lane 8a + b of instruction j: row 8j + a, 16-B chunk b ^ s(row), s(r) = (r >> 1) & 7),
+  // landing row-major in the wave's slot; lane r then reads its row's chunk c at position c ^ s(r),
+  // conflict-free (each 16-lane ds_read_b128 group covers 16 distinct 16-B bank slots). Per-lane
+  // register loads touch 64 lines per instruction, 16 B each, and need every line to stay in L1
+  // across the 8 instructions of a step.
+  unsigned char* ring = dyn_smem + wave * (SLOTS * 8192);
+  auto dma_line = [&](int slot, int item, int line) __attribute__((always_inline)) {
+    const int rows_here = min(64, n_rows - item * 64);  // rows past the end read as zeros
+    const __amdgpu_buffer_rsrc_t r =
+        tile_rsrc_u(corpus + (int64_t)item * 64 * row_stride, (uint32_t)(rows_here * row_stride));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 8 * j + (lane >> 3);
+      const uint32_t off = (uint32_t)(row * row_stride) + line * 128 + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+      blds16(r, off, ring + slot * 8192 + j * 1024);
+    }
+  };
+  // DMA: the fetch cursor runs SLOTS - 1 lines ahead of the current line; past the wave's last
+  // item it re-fetches the current line (every step issues the same 8 DMAs: counted vmcnt waits)
+  int slot = 0, fi = ci, fl = 0;
+  auto advance = [&](int& i, int& l) __attribute__((always_inline)) {
+    if (++l >= n_lines) {
+      l = 0;
+      i += W;
+    }
+  };
+  if (ci < i_end) {
+    if constexpr (DMA) {
+#pragma unroll
+      for (int t = 0; t < SLOTS - 1; ++t) {
+        const bool ok = fi < i_end;
+        dma_line(t, ok ? fi : ci, ok ? fl : 0);
+        advance(fi, fl);
+      }
+    } else {
+      load_line(A0, ci, 0);
+    }
+  }
   for (int i = tid; i < n_q * d_pad / 4; i += W * 64) {
     const int r = i / (d_pad / 4);
     const int c = i - r * (d_pad / 4);
@@ -2821,18 +2869,36 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
     thk[q] = 0;
     acc[q] = 0.f;
   }
-  auto step = [&](u32x4 (&C)[8 * LPS], u32x4 (&N)[8 * LPS]) __attribute__((always_inline)) {
-    int ni = ci, nl = cl + LPS;
+  auto step = [&](u32x4 (&C)[8], u32x4 (&N)[8]) __attribute__((always_inline)) {
+    int ni = ci, nl = cl + 1;
     if (nl >= n_lines) {
       nl = 0;
       ni += W;
     }
     {  // unconditional (a finished wave re-reads its current line): see topk_small_kernel
       const bool more = ni < i_end;
-      load_line(N, more ? ni : ci, more ? nl : cl);
+      if constexpr (DMA) {
+        asm volatile("" ::: "memory");  // the slot's reads of the previous step are consumed
+        const bool ok = fi < i_end;
+        int ws = slot + SLOTS - 1;
+        ws = ws >= SLOTS ? ws - SLOTS : ws;
+        dma_line(ws, ok ? fi : ci, ok ? fl : cl);
+        advance(fi, fl);
+        // this slot's 8 landed, the younger 8 (SLOTS - 1) in flight
+        if constexpr (SLOTS == 2)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        const unsigned char* src = ring + slot * 8192 + lane * 128;
+        const int sw = (lane >> 1) & 7;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) C[c] = *reinterpret_cast<const u32x4*>(src + ((c ^ sw) << 4));
+      } else {
+        load_line(N, more ? ni : ci, more ? nl : cl);
+      }
     }
 #pragma unroll
-    for (int g = 0; g < 4 * LPS; ++g) {  // 4 groups of 8 per line
+    for (int g = 0; g < 4; ++g) {  // 4 groups of 8 per line
       const f32x4 lo = __builtin_bit_cast(f32x4, C[2 * g]);
       const f32x4 hi = __builtin_bit_cast(f32x4, C[2 * g + 1]);
 #pragma unroll
@@ -2868,10 +2934,17 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
     }
     ci = ni;
     cl = nl;
+    slot = slot + 1 == SLOTS ? 0 : slot + 1;
     return ci < i_end;
   };
   if (ci < i_end) {
-    while (step(A0, A1) && step(A1, A0)) {
+    if constexpr (DMA) {
+      while (step(A0, A0)) {
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the finished wave's redundant line
+    } else {
+      while (step(A0, A1) && step(A1, A0)) {
+      }
     }
   }
   // per query: the wave's 64 lane lists -> one list (k rounds of a wave max) -> LDS; wave 0
@@ -2913,8 +2986,7 @@ __global__ __launch_bounds__(smallf32::kWaves * 64, 1) void topk_small_f32_kerne
     }
   }
   if (fold_ctr) {  // the last workgroup merges the splits (no merge launch)
-    extern __shared__ __attribute__((aligned(16))) unsigned char fold_smem[];
-    uint64_t* fl = reinterpret_cast<uint64_t*>(fold_smem);
+    uint64_t* fl = reinterpret_cast<uint64_t*>(dyn_smem);
     fold_last_arrival(part_keys, n_q, n_splits, k_out, fold_ctr, out_s, out_r, out_keys, fl,
                       reinterpret_cast<int*>(fl + (int64_t)n_q * n_splits * k_out));
   }
@@ -3681,22 +3753,28 @@ template <int KCAP>
 void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const FoldOut* fold,
                         hipStream_t s) {
   const int n_lines = (int)(ix->row_stride / 128);
-  const size_t lds = fold ? (size_t)B * p.n_splits * k * 8 + 16 : 0;
+  const size_t fold_lds = fold ? (size_t)B * p.n_splits * k * 8 + 16 : 0;
+  const int slots = smallf32::slots();
+  const size_t lds = std::max<size_t>(fold_lds, smallf32::ring_bytes(slots));
   uint32_t* fc = fold ? fold->ctr : nullptr;
   float* fs = fold ? fold->scores : nullptr;
   int32_t* fr = fold ? fold->rows : nullptr;
   uint64_t* fk = fold ? fold->keys : nullptr;
-#define AHR_F32_LAUNCH(NQ, LPS)                                                                                   \
-  hipLaunchKernelGGL((topk_small_f32_kernel<KCAP, NQ, LPS>), dim3((unsigned)p.n_splits), dim3(smallf32::kWaves * 64), \
-                     lds, s, ix->rows, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k,  \
-                     ix->part, fc, fs, fr, fk)
-  if (B == 1 && smallf32::lines_per_step(n_lines) == 2)
-    AHR_F32_LAUNCH(1, 2);
+  auto go = [&](auto kern, std::atomic<uint64_t>& attr) {
+    if (lds > 64 * 1024) ensure_lds_attr(attr, reinterpret_cast<const void*>(kern), (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(smallf32::waves_for(slots) * 64), lds, s, ix->rows,
+                       ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part, fc, fs,
+                       fr, fk);
+  };
+  static std::atomic<uint64_t> a12{0}, a42{0};
+  if (B == 1 && slots == 2)
+    go(topk_small_f32_kernel<KCAP, 1, 2>, a12);
   else if (B == 1)
-    AHR_F32_LAUNCH(1, 1);
+    go(topk_small_f32_kernel<KCAP, 1, 0>, a12);
+  else if (slots == 2)
+    go(topk_small_f32_kernel<KCAP, 4, 2>, a42);
   else
-    AHR_F32_LAUNCH(4, 1);
-#undef AHR_F32_LAUNCH
+    go(topk_small_f32_kernel<KCAP, 4, 0>, a42);
 }
 
 template <int DT>
