@@ -2607,9 +2607,11 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   const int split = blockIdx.x;
   const int pitch = (int)row_stride + small::kPitchPad;
 
-  const int n_blocks = (n_rows + 15) >> 4;
-  const int b_begin = (int)((int64_t)split * n_blocks / n_splits);
-  const int b_end = (int)((int64_t)(split + 1) * n_blocks / n_splits);
+  // the split's rows [r_begin, r_end): an equal share of the corpus, in 16-row blocks from r_begin
+  // (the last one may be partial: its rows past the split load the split's last row, unused)
+  const int r_begin = (int)((int64_t)split * n_rows / n_splits);
+  const int r_end = (int)((int64_t)(split + 1) * n_rows / n_splits);
+  const int b_end = (r_end - r_begin + 15) >> 4;
   // the wave's work is a sequence of items (16-row block, 8 k-steps); two register sets keep the
   // next item's loads in flight under the current item's MFMAs, across block boundaries
   // Every load is unconditional (steps past the row clamp to its last step; a finished wave
@@ -2618,7 +2620,7 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   // may not be in flight and waits vmcnt(0) before each MFMA, i.e. for the NEXT item's loads too,
   // which serialises the stream on one memory latency per item.
   auto load_item = [&](u32x4 (&A)[small::kKC], int blk, int s0) __attribute__((always_inline)) {
-    const uint8_t* arow = corpus + (int64_t)(blk * 16 + fr) * row_stride + fq * 16;
+    const uint8_t* arow = corpus + (int64_t)min(r_begin + blk * 16 + fr, r_end - 1) * row_stride + fq * 16;
 #pragma unroll
     for (int j = 0; j < small::kKC; ++j) {
       const int st = s0 + j < n_steps ? s0 + j : n_steps - 1;
@@ -2626,7 +2628,7 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
     }
   };
   u32x4 A0[small::kKC], A1[small::kKC];
-  int cb = b_begin + wave, cs = 0;
+  int cb = wave, cs = 0;
   if (cb < b_end) load_item(A0, cb, 0);  // in flight while the queries are staged
 
   // queries into LDS: converted from fp32 here (wave w: queries w, w + W, ...), or copied from
@@ -2682,12 +2684,12 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
         mfma16(a, *reinterpret_cast<const u32x4*>(qrow + 16 * g * pitch + st * 64), acc[g], DT);
     }
     if (ns == 0) {
-      const int r0 = cb * 16 + 4 * fq;
+      const int r0 = r_begin + cb * 16 + 4 * fq;
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          if (acc[g][i] >= thr[g] && r0 + i < n_rows) {
+          if (acc[g][i] >= thr[g] && r0 + i < r_end) {
             const uint64_t key = make_key(acc[g][i], row_base + (uint32_t)(r0 + i));
             if (key > thk[g]) {
               list_insert<KCAP>(L[g], key);
@@ -2800,15 +2802,17 @@ __global__ __launch_bounds__(smallf32::waves_for(SLOTS) * 64, 1) void topk_small
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int split = blockIdx.x;
-  const int n_items = (n_rows + 63) >> 6;
-  const int i_begin = (int)((int64_t)split * n_items / n_splits);
-  const int i_end = (int)((int64_t)(split + 1) * n_items / n_splits);
+  // the split's rows [r_begin, r_end): an equal share of the corpus (not whole 64-row items, so
+  // every CU streams the same bytes; the split's last item may be partial); items are local
+  const int r_begin = (int)((int64_t)split * n_rows / n_splits);
+  const int r_end = (int)((int64_t)(split + 1) * n_rows / n_splits);
+  const int i_end = (r_end - r_begin + 63) >> 6;
   const int d_pad = (int)(row_stride >> 2);
 
   u32x4 A0[8], A1[8];
-  int ci = i_begin + wave, cl = 0;  // current item, current 128-B line of the row
+  int ci = wave, cl = 0;  // current item, current 128-B line of the row
   auto load_line = [&](u32x4 (&A)[8], int item, int line) __attribute__((always_inline)) {
-    const int row = item * 64 + lane;
+    const int row = min(r_begin + item * 64 + lane, r_end - 1);  // past the split: its last row, unused
     const u32x4* src = reinterpret_cast<const u32x4*>(corpus + (int64_t)row * row_stride + line * 128);
 #pragma unroll
     for (int j = 0; j < 8; ++j) A[j] = src[j];
@@ -2821,9 +2825,10 @@ __global__ __launch_bounds__(smallf32::waves_for(SLOTS) * 64, 1) void topk_small
   // across the 8 instructions of a step.
   unsigned char* ring = dyn_smem + wave * (SLOTS * 8192);
   auto dma_line = [&](int slot, int item, int line) __attribute__((always_inline)) {
-    const int rows_here = min(64, n_rows - item * 64);  // rows past the end read as zeros
+    const int r0 = r_begin + item * 64;
+    const int rows_here = min(64, r_end - r0);  // rows past the split read as zeros
     const __amdgpu_buffer_rsrc_t r =
-        tile_rsrc_u(corpus + (int64_t)item * 64 * row_stride, (uint32_t)(rows_here * row_stride));
+        tile_rsrc_u(corpus + (int64_t)r0 * row_stride, (uint32_t)(rows_here * row_stride));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = 8 * j + (lane >> 3);
@@ -2919,10 +2924,10 @@ __global__ __launch_bounds__(smallf32::waves_for(SLOTS) * 64, 1) void topk_small
       }
     }
     if (nl == 0) {
-      const int row = ci * 64 + lane;
+      const int row = r_begin + ci * 64 + lane;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        if (q < n_q && row < n_rows) {
+        if (q < n_q && row < r_end) {
           const uint64_t key = make_key(acc[q], row_base + (uint32_t)row);
           if (key > thk[q]) {
             list_insert<KCAP>(L[q], key);

@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel trace + PMC passes (HBM bytes, MFMA busy) and their summary for one workload.
-# usage: bash tools/gpu/profile.sh OUTDIR WORKLOAD(hotpot90k|synth5m) [extra bench args]
+# usage: [BATCH=B] bash tools/gpu/profile.sh OUTDIR WORKLOAD(hotpot90k|hotpot90k_d384|synth5m) [extra bench args]
+# (BATCH: the batch the extra args give bench.py, e.g. BATCH=1 ... hotpot90k --dtype f32 --batch 1)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -8,5 +9,5 @@ O=$1; W=$2; shift 2
 mkdir -p $O
 if [ "$W" == "synth5m" ]; then STEPS="--steps 5 --warmup 2"; else STEPS="--steps 10 --warmup 3"; fi
 bash tools/profile_pmc.sh $O --workload $W $STEPS --no-cpu-baseline --inflight 1 --no-batch-sweep --no-f32-line --no-sublines "$@" || { echo PROFILE_FAILED; exit 1; }
-python tools/pmc_summary.py $O --workload $W --batch 1024 --out $O/pmc_traffic.json || exit 1
+python tools/pmc_summary.py $O --workload $W --batch ${BATCH:-1024} --out $O/pmc_traffic.json || exit 1
 cut -c1-800 $O/pmc_traffic.json

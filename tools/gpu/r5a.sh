@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 first GPU pass: full check, small-kernel A/B (previous vs current library), qres cost
-# split at d = 768 / 384 (ablation build), d = 384 PMC passes, clock-ramp A/B.
+# split at d = 768 / 384 (ablation build), d = 384 PMC passes, clock-ramp A/B. (For this pass the
+# ablation library was copied to _lib/abl/: _lib/ablation/ is in .gpurunignore.)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
