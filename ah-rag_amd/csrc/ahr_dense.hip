@@ -1987,30 +1987,55 @@ void launch_sample_kth(const float* scores, int B, int G, int k, float* thr, hip
 }
 
 // k-way merge when each lane holds one whole list in registers (n_lists <= 64, k_in <= KCAP):
-// no dependent global loads inside the k rounds.
+// no dependent global loads inside the k rounds. One wave per query, 4 queries per 256-thread
+// workgroup (B = 1024: 256 workgroups, not 1024 single-wave ones); a list comes in as 16-B loads
+// when k_in is even and the input 16-B aligned. A round's wave max runs on the keys' upper halves (the ordered scores: 32-bit
+// DPP max) and, only on a tie, on the lower halves of the tied lanes (keys are unique: distinct rows).
 template <int KCAP>
-__global__ __launch_bounds__(64) void merge_lane_lists_kernel(const uint64_t* __restrict__ in, int n_lists,
-                                                              int k_in, int k, float* __restrict__ scores,
-                                                              int32_t* __restrict__ rows,
-                                                              uint64_t* __restrict__ keys_out) {
-  const int q = blockIdx.x;
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(256) void merge_lane_lists_kernel(const uint64_t* __restrict__ in, int n_q,
+                                                               int n_lists, int k_in, int k, int vec16,
+                                                               float* __restrict__ scores,
+                                                               int32_t* __restrict__ rows,
+                                                               uint64_t* __restrict__ keys_out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= n_q) return;  // wave-uniform
   const uint64_t* src = in + ((int64_t)q * n_lists + lane) * k_in;
   uint64_t L[KCAP];
   // a list ends at its first empty slot (key 0): the register-resident kernel writes only its kept
   // keys and one terminating 0 (kFlagShortLists), so the slots after it hold another launch's keys
+  if (vec16) {  // k_in even, 16-B aligned input
+#pragma unroll
+    for (int j = 0; j < KCAP; j += 2) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (lane < n_lists && j < k_in) v = *reinterpret_cast<const u32x4*>(src + j);
+      L[j] = ((uint64_t)v[1] << 32) | v[0];
+      L[j + 1] = ((uint64_t)v[3] << 32) | v[2];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < KCAP; ++j) L[j] = (lane < n_lists && j < k_in) ? src[j] : 0;
+  }
   bool end = false;
 #pragma unroll
   for (int j = 0; j < KCAP; ++j) {
-    const uint64_t v = (lane < n_lists && j < k_in) ? src[j] : 0;
-    end = end || v == 0;
-    L[j] = end ? 0 : v;
+    end = end || L[j] == 0;
+    L[j] = end ? 0 : L[j];
   }
   // lane j keeps output j (k <= 64): one coalesced store per output array at the end instead of a
   // lane-0 store per round
   uint64_t mine = 0;
   for (int j = 0; j < k; ++j) {
-    const uint64_t best = wave_max_u64(L[0]);
+    const uint32_t hi = (uint32_t)(L[0] >> 32);
+    const uint32_t mh = dpp_max_u32(hi);
+    const uint64_t tied = __ballot(hi == mh);
+    uint64_t best;
+    if (__popcll(tied) == 1) {  // wave-uniform
+      best = readlane_u64(L[0], __ffsll((unsigned long long)tied) - 1);
+    } else {
+      const uint32_t ml = dpp_max_u32(hi == mh ? (uint32_t)L[0] : 0u);
+      best = ((uint64_t)mh << 32) | ml;
+    }
     if (best != 0 && L[0] == best) {
 #pragma unroll
       for (int t = 0; t < KCAP - 1; ++t) L[t] = L[t + 1];
@@ -3893,12 +3918,13 @@ void launch_merge(const uint64_t* in, int B, int n_lists, int k_in, int k, float
                   int32_t* rows, uint64_t* keys_out, hipStream_t s) {
   if (n_lists <= 64 && k_in <= 32) {
     const int kc = kcap_for(k_in);
+    const int vec16 = (k_in % 2 == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0) ? 1 : 0;
     if (kc == 8)
-      hipLaunchKernelGGL((merge_lane_lists_kernel<8>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+      hipLaunchKernelGGL((merge_lane_lists_kernel<8>), dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, in, B, n_lists, k_in, k, vec16, scores, rows, keys_out);
     else if (kc == 16)
-      hipLaunchKernelGGL((merge_lane_lists_kernel<16>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+      hipLaunchKernelGGL((merge_lane_lists_kernel<16>), dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, in, B, n_lists, k_in, k, vec16, scores, rows, keys_out);
     else
-      hipLaunchKernelGGL((merge_lane_lists_kernel<32>), dim3(B), dim3(64), 0, s, in, n_lists, k_in, k, scores, rows, keys_out);
+      hipLaunchKernelGGL((merge_lane_lists_kernel<32>), dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, in, B, n_lists, k_in, k, vec16, scores, rows, keys_out);
     return;
   }
   if (n_lists <= 512 && n_lists * k_in <= kMergeBlockKeys) {

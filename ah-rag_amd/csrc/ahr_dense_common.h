@@ -85,6 +85,27 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, false);
+}
+// wave64 max of u32 values (the DPP sequence of wave_max_u64), in every lane
+__device__ __forceinline__ uint32_t dpp_max_u32(uint32_t x) {
+  x = max(x, dpp_u32<0x111, 0xf>(x));  // row_shr:1
+  x = max(x, dpp_u32<0x112, 0xf>(x));  // row_shr:2
+  x = max(x, dpp_u32<0x114, 0xf>(x));  // row_shr:4
+  x = max(x, dpp_u32<0x118, 0xf>(x));  // row_shr:8
+  x = max(x, dpp_u32<0x142, 0xa>(x));  // row_bcast:15
+  x = max(x, dpp_u32<0x143, 0xc>(x));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
   const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);

@@ -91,21 +91,6 @@ __device__ __forceinline__ bool in_sched(uint32_t mask, int bi, int off) {
   return bi < 32 ? ((mask >> bi) & 1) != 0 : (bi + off) % (bi < 128 ? 8 : 128) == 0;
 }
 
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, false);
-}
-// wave64 max of u32 values (the DPP sequence of wave_max_u64), in every lane
-__device__ __forceinline__ uint32_t dpp_max_u32(uint32_t x) {
-  x = max(x, dpp_u32<0x111, 0xf>(x));  // row_shr:1
-  x = max(x, dpp_u32<0x112, 0xf>(x));  // row_shr:2
-  x = max(x, dpp_u32<0x114, 0xf>(x));  // row_shr:4
-  x = max(x, dpp_u32<0x118, 0xf>(x));  // row_shr:8
-  x = max(x, dpp_u32<0x142, 0xa>(x));  // row_bcast:15
-  x = max(x, dpp_u32<0x143, 0xc>(x));  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
 // k-th largest of the wave's nonzero values (lane l holds v0, v1); 0 if fewer than k are nonzero.
 // k rounds of a wave max, each removing one instance (the lowest lane holding it).
 __device__ __forceinline__ uint32_t wave_kth(uint32_t v0, uint32_t v1, int k, int lane) {
