@@ -2813,7 +2813,8 @@ inline int waves_per_split() {
 
 template <int KCAP, int NQ, int SLOTS>
 __global__ __launch_bounds__(smallf32::waves_for(SLOTS) * 64, 1) void topk_small_f32_kernel(
-    const uint8_t* __restrict__ corpus, const uint8_t* __restrict__ qconv, int64_t row_stride, int n_rows, int n_q,
+    const uint8_t* __restrict__ corpus, const float* __restrict__ qsrc, int dim, int normalize,
+    const uint8_t* __restrict__ qconv, int64_t row_stride, int n_rows, int n_q,
     int n_lines, int n_splits, uint32_t row_base, int k_out, uint64_t* __restrict__ part_keys,
     uint32_t* __restrict__ fold_ctr, float* __restrict__ out_s, int32_t* __restrict__ out_r,
     uint64_t* __restrict__ out_keys) {
@@ -2882,10 +2883,43 @@ __global__ __launch_bounds__(smallf32::waves_for(SLOTS) * 64, 1) void topk_small
       load_line(A0, ci, 0);
     }
   }
-  for (int i = tid; i < n_q * d_pad / 4; i += W * 64) {
-    const int r = i / (d_pad / 4);
-    const int c = i - r * (d_pad / 4);
-    reinterpret_cast<f32x4*>(qs)[r * 256 + c] = *reinterpret_cast<const f32x4*>(qconv + (int64_t)r * row_stride + c * 16);
+  if (qsrc) {  // queries converted here (wave r: query r), convert_rows_kernel's fp32 arithmetic
+    for (int r = wave; r < n_q; r += W) {
+      const float* x = qsrc + (int64_t)r * dim;
+      const bool vec = (dim & 3) == 0;
+      float nrm = 1.f;
+      if (normalize) {
+        float sq = 0.f;
+        if (vec) {
+          for (int j = 4 * lane; j < dim; j += 256) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(x + j);
+            sq = fmaf(v[0], v[0], sq); sq = fmaf(v[1], v[1], sq); sq = fmaf(v[2], v[2], sq); sq = fmaf(v[3], v[3], sq);
+          }
+        } else {
+          for (int j = lane; j < dim; j += 64) sq = fmaf(x[j], x[j], sq);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
+        nrm = fmaxf(sqrtf(sq), 1e-12f);
+      }
+      for (int j = 4 * lane; j < d_pad; j += 256) {
+        f32x4 v;
+        if (vec && j + 3 < dim) {
+          v = *reinterpret_cast<const f32x4*>(x + j);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = (j + u < dim) ? x[j + u] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) qs[r * 1024 + f32_perm(j + u)] = normalize ? v[u] / nrm : v[u];
+      }
+    }
+  } else {
+    for (int i = tid; i < n_q * d_pad / 4; i += W * 64) {
+      const int r = i / (d_pad / 4);
+      const int c = i - r * (d_pad / 4);
+      reinterpret_cast<f32x4*>(qs)[r * 256 + c] = *reinterpret_cast<const f32x4*>(qconv + (int64_t)r * row_stride + c * 16);
+    }
   }
   __syncthreads();
 
@@ -3778,10 +3812,12 @@ void launch_small_k(const ahr_index* ix, const SearchPlan& p, const float* q, in
 inline bool small_fuses_convert(const ahr_index* ix) {
   return ix->dtype != AHR_F32 && (ix->dim & 3) == 0 && ix->d_pad <= 1024;
 }
+// fp32: topk_small_f32_kernel always converts its queries itself (convert_rows_kernel's arithmetic)
+inline bool small_plan_fuses_convert(const ahr_index* ix) { return ix->dtype == AHR_F32 || small_fuses_convert(ix); }
 
 template <int KCAP>
-void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const FoldOut* fold,
-                        hipStream_t s) {
+void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t row_base, const float* q,
+                        int normalize_q, const FoldOut* fold, hipStream_t s) {
   const int n_lines = (int)(ix->row_stride / 128);
   const size_t fold_lds = fold ? (size_t)B * p.n_splits * k * 8 + 16 : 0;
   const int slots = smallf32::slots();
@@ -3792,9 +3828,9 @@ void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, 
   uint64_t* fk = fold ? fold->keys : nullptr;
   auto go = [&](auto kern, std::atomic<uint64_t>& attr) {
     if (lds > 64 * 1024) ensure_lds_attr(attr, reinterpret_cast<const void*>(kern), (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(smallf32::waves_for(slots) * 64), lds, s, ix->rows,
-                       ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base, k, ix->part, fc, fs,
-                       fr, fk);
+    hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(smallf32::waves_for(slots) * 64), lds, s, ix->rows, q,
+                       ix->dim, normalize_q, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base,
+                       k, ix->part, fc, fs, fr, fk);
   };
   static std::atomic<uint64_t> a12{0}, a42{0};
   if (B == 1 && slots == 2)
@@ -3816,11 +3852,11 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     if (p.kernel == KERNEL_SMALL) {
       prof_mark(ix, 2, s);
       if (k <= 8)
-        launch_small_f32_k<8>(ix, p, B, k, row_base, fold, s);
+        launch_small_f32_k<8>(ix, p, B, k, row_base, q, normalize_q, fold, s);
       else if (k <= 12)
-        launch_small_f32_k<12>(ix, p, B, k, row_base, fold, s);
+        launch_small_f32_k<12>(ix, p, B, k, row_base, q, normalize_q, fold, s);
       else
-        launch_small_f32_k<16>(ix, p, B, k, row_base, fold, s);
+        launch_small_f32_k<16>(ix, p, B, k, row_base, q, normalize_q, fold, s);
       return;
     }
   } else {
@@ -4029,7 +4065,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
       frag_done = true;
     }
   }
-  if (!frag_done && !(small_plan && small_fuses_convert(ix)))
+  if (!frag_done && !(small_plan && small_plan_fuses_convert(ix)))
     hipLaunchKernelGGL(convert_rows_kernel, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, s, q,
                        (int64_t)B, ix->dim, (const int64_t*)nullptr, (int64_t)0, normalize_q, ix->qbuf,
                        ix->row_stride, ix->d_pad, ix->dtype);

@@ -14,5 +14,5 @@ for r in $(seq 1 $R); do for lib in "$@"; do
   AHR_LIB_PATH=$lib timeout -k 10 300 python -u tools/small_ab.py --batches 1,4 --reps 100 > $O/ab_${v}_r$r.json 2> $O/ab_${v}_r$r.err || { echo AB_FAIL; tail -5 $O/ab_${v}_r$r.err; exit 1; }
   python -c "
 import json,sys; d=json.load(open(sys.argv[1]))
-print(sys.argv[2], *[(b, d[b]['warm_us'].get('tile_topk'), d[b]['cold_us'].get('tile_topk')) for b in ('f32_b1','f32_b4','bf16_b1','bf16_b4')])" $O/ab_${v}_r$r.json $v
+print(sys.argv[2], *[(b, d[b]['warm_us'].get('tile_topk'), d[b]['cold_us'].get('tile_topk'), 'sum', round(sum(d[b]['warm_us'].values()), 2)) for b in ('f32_b1','f32_b4','bf16_b1','bf16_b4')])" $O/ab_${v}_r$r.json $v
 done; done
