@@ -2606,15 +2606,27 @@ constexpr int kPitchPad = 16;  // query rows in LDS: pitch = row bytes + 16 (con
 // with 8 waves, 42.9 k / 516 k with 12, 38.2 k / 471 k with 16 — a 16-wave workgroup fills a CU's
 // VGPRs, so the other batch's kernel cannot co-reside; serial latency 8 % higher with 8)
 __host__ __device__ constexpr int waves(int ng) { return ng == 1 ? AHR_SMALL_WAVES : 8; }
-// LDS: the NG * 16 query rows, later overlaid by one group's lane lists (16 x 4 W x KCAP keys)
-inline int lds_bytes(int64_t row_stride, int kcap, int ng) {
-  const int64_t q = (int64_t)16 * ng * (row_stride + kPitchPad);
+// LDS: the NG * 16 query rows (then, in the DMA form, the line ring: W waves x 2 slots x 8 KiB),
+// later overlaid by one group's lane lists (16 x 4 W x KCAP keys)
+__host__ __device__ inline int q_region(int64_t row_stride, int ng) {
+  return (int)(((int64_t)16 * ng * (row_stride + kPitchPad) + 15) & ~(int64_t)15);
+}
+inline int lds_bytes(int64_t row_stride, int kcap, int ng, bool dma = false) {
+  const int64_t q = q_region(row_stride, ng) + (dma ? (int64_t)waves(ng) * 2 * 8192 : 0);
   const int64_t l = (int64_t)16 * 4 * waves(ng) * kcap * 8;
   return (int)(q > l ? q : l);
 }
+// the DMA form (A/B: AHR_SMALL_DMA=1) where it fits 160 KiB of LDS
+inline bool use_dma(int64_t row_stride, int ng) {
+  static const bool on = [] {
+    const char* e = getenv("AHR_SMALL_DMA");
+    return e && atoi(e) != 0;
+  }();
+  return on && ng == 1 && q_region(row_stride, ng) + waves(ng) * 2 * 8192 <= 160 * 1024;
+}
 }  // namespace small
 
-template <int DT, int KCAP, int NG>
+template <int DT, int KCAP, int NG, bool DMA>
 __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
     const uint8_t* __restrict__ corpus, const float* __restrict__ qsrc, int dim, int normalize,
     const uint8_t* __restrict__ qconv, int64_t row_stride, int d_pad, int n_rows, int n_q, int n_steps,
@@ -2644,6 +2656,23 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   // loads: with a conditional load the compiler's waitcnt placement must assume the younger item
   // may not be in flight and waits vmcnt(0) before each MFMA, i.e. for the NEXT item's loads too,
   // which serialises the stream on one memory latency per item.
+  // DMA form (AHR_SMALL_DMA=1, one workgroup per CU): an item (16 rows x 8 steps x 64 B) comes in
+  // by LDS-DMA as 8 wave-instructions of 2 rows x 512 B each into a two-slot per-wave ring after
+  // the query rows (row-major, 16-B chunk c of a row at position c ^ (row & 15): the fragment
+  // reads below are conflict-free); the register form's loads touch 16 half-lines per instruction.
+  unsigned char* ring = smem + small::q_region(row_stride, NG) + wave * (2 * 8192);
+  auto dma_item = [&](int sl, int blk, int s0) __attribute__((always_inline)) {
+    const int r0 = r_begin + blk * 16;
+    const int rows_here = min(16, r_end - r0);  // rows past the split read as zeros
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc_u(corpus + (int64_t)r0 * row_stride, (uint32_t)(rows_here * row_stride));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 2 * j + (lane >> 5);
+      const uint32_t off = (uint32_t)(row * row_stride) + s0 * 64 + (((lane & 31) ^ (row & 15)) << 4);
+      blds16(r, off, ring + sl * 8192 + j * 1024);
+    }
+  };
+  int slot = 0;
   auto load_item = [&](u32x4 (&A)[small::kKC], int blk, int s0) __attribute__((always_inline)) {
     const uint8_t* arow = corpus + (int64_t)min(r_begin + blk * 16 + fr, r_end - 1) * row_stride + fq * 16;
 #pragma unroll
@@ -2654,7 +2683,12 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
   };
   u32x4 A0[small::kKC], A1[small::kKC];
   int cb = wave, cs = 0;
-  if (cb < b_end) load_item(A0, cb, 0);  // in flight while the queries are staged
+  if (cb < b_end) {  // in flight while the queries are staged
+    if constexpr (DMA)
+      dma_item(0, cb, 0);
+    else
+      load_item(A0, cb, 0);
+  }
 
   // queries into LDS: converted from fp32 here (wave w: queries w, w + W, ...), or copied from
   // the query buffer
@@ -2696,7 +2730,16 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
     }
     {
       const bool more = nb < b_end;
-      load_item(N, more ? nb : cb, more ? ns : cs);
+      if constexpr (DMA) {
+        asm volatile("" ::: "memory");  // the slot's reads of the previous step are consumed
+        dma_item(slot ^ 1, more ? nb : cb, more ? ns : cs);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this slot landed, the next one in flight
+        const unsigned char* src = ring + slot * 8192 + fr * 512;
+#pragma unroll
+        for (int j = 0; j < small::kKC; ++j) C[j] = *reinterpret_cast<const u32x4*>(src + (((j * 4 + fq) ^ fr) << 4));
+      } else {
+        load_item(N, more ? nb : cb, more ? ns : cs);
+      }
     }
 #pragma unroll
     for (int j = 0; j < small::kKC; ++j) {
@@ -2728,10 +2771,17 @@ __global__ __launch_bounds__(small::waves(NG) * 64, 1) void topk_small_kernel(
     }
     cb = nb;
     cs = ns;
+    slot ^= 1;
     return cb < b_end;
   };
   if (cb < b_end) {
-    while (step(A0, A1) && step(A1, A0)) {
+    if constexpr (DMA) {
+      while (step(A0, A0)) {
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the finished wave's redundant item
+    } else {
+      while (step(A0, A1) && step(A1, A0)) {
+      }
     }
   }
 
@@ -3785,16 +3835,25 @@ struct FoldOut {
 template <int DT, int KCAP, int NG>
 void launch_small(const ahr_index* ix, const SearchPlan& p, const float* q, int normalize_q, int B, int k,
                   uint32_t row_base, const FoldOut* fold, hipStream_t s) {
-  constexpr auto kern = &topk_small_kernel<DT, KCAP, NG>;
-  int lds = small::lds_bytes(ix->row_stride, KCAP, NG);
+  const bool dma = small::use_dma(ix->row_stride, NG);
+  int lds = small::lds_bytes(ix->row_stride, KCAP, NG, dma);
   if (fold) lds = std::max(lds, B * p.n_splits * k * 8 + 16);
-  static std::atomic<uint64_t> lds_attr{0};  // > 64 KiB dynamic LDS: opt in per device
-  ensure_lds_attr(lds_attr, reinterpret_cast<const void*>(kern), 160 * 1024);
-  hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::waves(NG) * 64), lds, s, ix->rows, q, ix->dim,
-                     normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, (int)ix->count, B,
-                     (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part,
-                     fold ? fold->ctr : nullptr, fold ? fold->scores : nullptr, fold ? fold->rows : nullptr,
-                     fold ? fold->keys : nullptr);
+  auto go = [&](auto kern, std::atomic<uint64_t>& attr) {
+    ensure_lds_attr(attr, reinterpret_cast<const void*>(kern), 160 * 1024);  // > 64 KiB: opt in per device
+    hipLaunchKernelGGL(kern, dim3((unsigned)p.n_splits), dim3(small::waves(NG) * 64), lds, s, ix->rows, q, ix->dim,
+                       normalize_q, ix->qbuf, ix->row_stride, ix->d_pad, (int)ix->count, B,
+                       (int)(ix->d_pad * ix->elem / 64), p.n_splits, row_base, k, ix->part,
+                       fold ? fold->ctr : nullptr, fold ? fold->scores : nullptr, fold ? fold->rows : nullptr,
+                       fold ? fold->keys : nullptr);
+  };
+  static std::atomic<uint64_t> a_reg{0}, a_dma{0};
+  if constexpr (NG == 1) {
+    if (dma) {
+      go(&topk_small_kernel<DT, KCAP, NG, true>, a_dma);
+      return;
+    }
+  }
+  go(&topk_small_kernel<DT, KCAP, NG, false>, a_reg);
 }
 
 template <int DT, int NG>
