@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from ..graph.hierarchical_graph import HierarchicalGraph
-from ..graph_search import parse_judge
+from ..graph_search import parse_judge, to_host_arrays
 
 ADJ_BT_OUT, ADJ_BT_IN = 0, 1
 
@@ -350,14 +350,14 @@ def lca_batch(hg: HierarchicalGraph, inputs: Sequence[Sequence[str]]) -> List[Li
         if ids:
             idx[b, :len(ids)] = dg.node_indices(ids)
     out, cnt = dg.lca(torch.from_numpy(idx))
-    out_h, cnt_h = out.cpu().numpy(), cnt.cpu().numpy()
+    out_h, cnt_h = to_host_arrays(out, cnt)
     res = [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] if cnt_h[b] >= 0 else None for b in range(len(inputs))]
     over = np.nonzero(cnt_h < 0)[0]
     if len(over):
         # ancestor sets beyond the LDS kernel's capacity (4096 visited nodes, 1024 per level):
         # the global-memory form of the same walk answers those queries (ahr_graph_lca_large)
         out2, cnt2 = dg.lca_large(torch.from_numpy(idx[over]))
-        out2_h, cnt2_h = out2.cpu().numpy(), cnt2.cpu().numpy()
+        out2_h, cnt2_h = to_host_arrays(out2, cnt2)
         for j, b in enumerate(over):
             if cnt2_h[j] < 0:
                 raise RuntimeError("ahr_graph_lca_large reported an overflow with max_out = n_nodes")
@@ -375,5 +375,5 @@ def expand_batch(hg: HierarchicalGraph, action: str, inputs: Sequence[Sequence[s
         if ids:
             idx[b, :len(ids)] = dg.node_indices(ids)
     out, cnt = dg.expand(action, torch.from_numpy(idx), limit)
-    out_h, cnt_h = out.cpu().numpy(), cnt.cpu().numpy()
+    out_h, cnt_h = to_host_arrays(out, cnt)
     return [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] for b in range(len(inputs))]

@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from ..graph.hierarchical_graph import HierarchicalGraph
-from ..graph_search import parse_judge
+from ..graph_search import parse_judge, to_host_arrays
 from .environment import GraphEnvironment
 from .featurizer import NODE_FEATS, featurize_observation
 from .gym_env import END_EPISODE, N_ACTIONS, TOP_IDS
@@ -361,8 +361,7 @@ class VecAHRAGGymEnv:
             t = TOP_IDS[act]
             inp = np.where(top_valid[g, :t] & (prev.sel[g, :t] < n_graph), prev.sel[g, :t], -1)
             out, cnt = self._engine.graph.expand(name, torch.from_numpy(inp.astype(np.int32)), K_NODES)
-            out_h = out.cpu().numpy().astype(np.int64)
-            cnt_h = cnt.cpu().numpy().astype(np.int64)
+            out_h, cnt_h = (a.astype(np.int64) for a in to_host_arrays(out, cnt))
             self._steps[g] += 1
             ob.kind[g] = OBS_EXPAND
             ob.step[g] = self._steps[g]

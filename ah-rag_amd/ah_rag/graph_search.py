@@ -161,24 +161,21 @@ class DeviceGraph:
         max_exp = max(1, k * (1 + fan))
         top_k = max(params.top_k, 0)
         kk = max(top_k, 1)
-        en = torch.empty((B, max_exp), dtype=torch.int32, device=dev)
-        es = torch.empty((B, max_exp), dtype=torch.float64, device=dev)
-        ex = torch.empty((B, max_exp), dtype=torch.int32, device=dev)
-        ec = torch.empty((B,), dtype=torch.int32, device=dev)
-        on = torch.empty((B, kk), dtype=torch.int32, device=dev)
-        osem = torch.empty((B, kk), dtype=torch.float64, device=dev)
-        osc = torch.empty((B, kk), dtype=torch.float64, device=dev)
-        oc = torch.empty((B,), dtype=torch.int32, device=dev)
+        # the eight outputs as views of one device arena: one host copy brings them all back
+        arena, (en, es, ex, ec, on, osem, osc, oc) = _arena(dev, [
+            ((B, max_exp), torch.int32), ((B, max_exp), torch.float64), ((B, max_exp), torch.int32),
+            ((B,), torch.int32), ((B, kk), torch.int32), ((B, kk), torch.float64), ((B, kk), torch.float64),
+            ((B,), torch.int32)])
         c = params.to_c()
         sn = seed_nodes.to(device=dev, dtype=torch.int32).contiguous()
         ss = seed_sem.to(device=dev, dtype=torch.float32).contiguous()
-        _on_stream(stream, dev, sn, ss, en, es, ex, ec, on, osem, osc, oc)
+        _on_stream(stream, dev, sn, ss, arena)
         with torch.cuda.device(dev):
             nat.check(nat.lib().ahr_graph_expand_rerank(
                 self._h, nat.ptr(sn), nat.ptr(ss), B, k, nat.ctypes.byref(c), max_exp,
                 nat.ptr(en), nat.ptr(es), nat.ptr(ex), nat.ptr(ec), nat.ptr(on), nat.ptr(osem),
                 nat.ptr(osc), nat.ptr(oc), nat.stream_ptr(stream)), "ahr_graph_expand_rerank")
-        return RerankResult(en, es, ex, ec, on, osem, osc, oc)
+        return RerankResult(en, es, ex, ec, on, osem, osc, oc, arena)
 
     def lca(self, inputs: torch.Tensor, max_out: int = 1024,
             stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -230,10 +227,9 @@ class DeviceGraph:
         """Batched environment expansion: inputs int32 [B, n_in] node indices (-1 = skip)."""
         B, n_in = inputs.shape
         dev = self.device
-        out = torch.empty((B, max(limit, 1)), dtype=torch.int32, device=dev)
-        cnt = torch.empty((B,), dtype=torch.int32, device=dev)
+        arena, (out, cnt) = _arena(dev, [((B, max(limit, 1)), torch.int32), ((B,), torch.int32)])
         x = inputs.to(device=dev, dtype=torch.int32).contiguous()
-        _on_stream(stream, dev, x, out, cnt)
+        _on_stream(stream, dev, x, arena)
         with torch.cuda.device(dev), devtime.span(stream, dev):
             nat.check(nat.lib().ahr_graph_expand(self._h, ACTIONS[action], nat.ptr(x), B, n_in, int(limit),
                                                  nat.ptr(out), nat.ptr(cnt), nat.stream_ptr(stream)),
@@ -284,11 +280,71 @@ class RerankResult:
     out_sem: torch.Tensor
     out_score: torch.Tensor
     out_count: torch.Tensor
+    arena: Optional[torch.Tensor] = None  # the device buffer the eight outputs are views of
 
-    def to_host(self) -> "RerankResult":
-        return RerankResult(*[t.cpu().numpy() for t in (self.exp_nodes, self.exp_sem, self.exp_src,
-                                                        self.exp_count, self.out_nodes, self.out_sem,
-                                                        self.out_score, self.out_count)])
+    def to_host(self, *extra: torch.Tensor):
+        """The result as host arrays (and `extra` tensors after it), one stream sync for all."""
+        arrs = to_host_arrays(self.exp_nodes, self.exp_sem, self.exp_src, self.exp_count, self.out_nodes,
+                              self.out_sem, self.out_score, self.out_count, *extra)
+        res = RerankResult(*arrs[:8])
+        return (res, *arrs[8:]) if extra else res
+
+
+_ELEM = {torch.int32: (4, np.int32), torch.float64: (8, np.float64), torch.float32: (4, np.float32),
+         torch.int64: (8, np.int64), torch.uint8: (1, np.uint8)}
+
+
+def _arena(dev: torch.device, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]]):
+    """One uninitialised device buffer holding tensors of the given (shape, dtype)s, each at an
+    8-byte aligned offset: (buffer, views)."""
+    offs, sizes, total = [], [], 0
+    for shape, dt in specs:
+        n = math.prod(shape) * _ELEM[dt][0]
+        offs.append(total)
+        sizes.append(n)
+        total += (n + 7) // 8 * 8
+    buf = torch.empty(max(total, 8), dtype=torch.uint8, device=dev)
+    views = []
+    for (shape, dt), o, n in zip(specs, offs, sizes):
+        v = buf[o:o + n].view(dt).view(shape)
+        v._ahr_arena = (buf, o)  # (a dtype view is not tracked as a view of buf: to_host_arrays)
+        views.append(v)
+    return buf, views
+
+
+def to_host_arrays(*tensors: torch.Tensor) -> List[np.ndarray]:
+    """Device tensors -> numpy with one synchronisation: asynchronous copies into pinned host
+    memory on the current stream, then one wait (a .cpu() per tensor waits once per tensor; the
+    single-environment loop made ~14 such round trips per episode). Views of one _arena buffer
+    come back with one copy of that buffer."""
+    if not tensors:
+        return []
+    dev = tensors[0].device
+    if dev.type != "cuda":
+        return [t.numpy() for t in tensors]
+    srcs: Dict[int, torch.Tensor] = {}
+    plan = []
+    for t in tensors:
+        ar = getattr(t, "_ahr_arena", None)
+        if ar is not None:
+            base, o = ar
+            srcs.setdefault(id(base), base)
+            plan.append((id(base), (o, t)))
+        else:
+            srcs[id(t)] = t
+            plan.append((id(t), None))
+    host = {k: v.to("cpu", non_blocking=True) for k, v in srcs.items()}
+    torch.cuda.current_stream(dev).synchronize()
+    host = {k: v.numpy() for k, v in host.items()}
+    out = []
+    for key, view in plan:
+        if view is None:
+            out.append(host[key])
+            continue
+        o, t = view
+        esz, npt = _ELEM[t.dtype]
+        out.append(host[key][o:o + t.numel() * esz].view(npt).reshape(tuple(t.shape)))
+    return out
 
 
 def resolve_search_params(stored: Dict[str, Any], top_k: int, member_top_m: Optional[int],
@@ -346,5 +402,5 @@ class SearchEngine:
             res = self.graph.expand_rerank(nodes, scores, params, stream=stream)
             if stream is not None:
                 torch.cuda.current_stream(self.graph.device).wait_stream(stream)
-        host = res.to_host()
-        return rows.cpu().numpy(), scores.cpu().numpy(), host
+        host, rows_h, scores_h = res.to_host(rows, scores)
+        return rows_h, scores_h, host

@@ -476,7 +476,7 @@ def env_line(args, dev, rank: int = 0, world: int = 1) -> dict:
     cpu_fn = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu_fn = lambda *x: cpu_env_baseline(*x, budget_s=max(4.0, args.cpu_seconds))  # noqa: E731
-    return bench_env.measure(dev, args.envs, 6, single=32, rank=rank, world=world, total_envs=args.envs * world,
+    return bench_env.measure(dev, args.envs, 6, single=64, rank=rank, world=world, total_envs=args.envs * world,
                              backend=args.backend, episodes=max(1, args.episodes), cpu_baseline_fn=cpu_fn)
 
 

@@ -59,7 +59,7 @@ def single_reset(env: AHRAGGymEnv, hg, query: str, qvec: np.ndarray):
     return env._finish_reset(obs)
 
 
-def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: int = 1, total_envs=None,
+def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: int = 1, total_envs=None,
             backend: str = "nccl", episodes: int = 5, cpu_baseline_fn=None) -> dict:
     """One rank's C5 measurement: build the graph, then a warm-up episode and `episodes` timed
     batched VecAHRAGGymEnv episodes of `envs` environments (reset + `steps` steps of random valid
@@ -128,7 +128,11 @@ def measure(dev, envs: int, steps: int, single: int = 32, rank: int = 0, world: 
         n1 = min(single, envs)
         env = AHRAGGymEnv(max_steps=steps + 1, graph=hg)
         env.env.logging_enabled = False
-        hg.search_batch(queries[:1], top_k=5, return_cluster=True, query_vectors=qv[:1])
+        for i in range(2):  # warm-up episodes: every action kind's first call, the host allocator
+            single_reset(env, hg, queries[-1 - i], qv[-1 - i:len(qv) - i])
+            for a in (0, 1, 2, 3, 4, 0):
+                env.step(a if env.get_action_mask()[a] else random_actions(rng, [env.get_action_mask()])[0])
+        torch.cuda.synchronize()
         ts = time.perf_counter()
         for i in range(n1):
             # reset with a precomputed vector (the search at B = 1)
@@ -194,7 +198,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--envs", type=int, default=1024, help="environments of the whole job")
     ap.add_argument("--steps", type=int, default=6)
-    ap.add_argument("--single", type=int, default=32, help="environments stepped one by one (rank 0)")
+    ap.add_argument("--single", type=int, default=64, help="environments stepped one by one (rank 0)")
     ap.add_argument("--episodes", type=int, default=5, help="timed episodes after the warm-up one")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="host baseline budget (rank 0; 0 = off): bench.cpu_env_baseline")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl")

@@ -1,0 +1,69 @@
+"""cProfile of the drop-in single-environment loop on the C5 workload (diagnostic).
+
+AHRAGGymEnv stepped one environment at a time (tools/bench_env.py's `single` leg: reset at B = 1
+with a precomputed query vector, then random valid actions), profiled over --envs episodes after
+one warm-up episode; prints the wall rate and the top functions by own and cumulative time.
+usage: python tools/profile_single_env.py [--envs 64] [--steps 6]
+"""
+import argparse
+import cProfile
+import io
+import os
+import pstats
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ah-rag_amd"), ROOT, os.path.join(ROOT, "tools")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench_env  # noqa: E402
+from ah_rag.agent.gym_env import AHRAGGymEnv  # noqa: E402
+from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph, install_vectors  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=6)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(7)
+    corpus = SyntheticCorpus(HOTPOT_90K, dev)
+    vectors = corpus.rows().cpu().numpy()
+    hg, ids = build_hotpot_graph(corpus, np.random.default_rng(20251003))
+    install_vectors(hg, ids, vectors, os.path.join(tempfile.mkdtemp(prefix="ahr_single_"), "vector_db"))
+    q, _ = corpus.queries(a.envs + 1, corpus.rows())
+    qv = q.cpu().numpy()
+    env = AHRAGGymEnv(max_steps=a.steps + 1, graph=hg)
+    env.env.logging_enabled = False
+
+    def episode(i):
+        bench_env.single_reset(env, hg, f"q{i}", qv[i:i + 1])
+        for _ in range(a.steps):
+            env.step(bench_env.random_actions(rng, [env.get_action_mask()])[0])
+
+    episode(a.envs)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.envs):
+        episode(i)
+    wall = time.perf_counter() - t0
+    prof = cProfile.Profile()
+    prof.enable()
+    for i in range(a.envs):
+        episode(i)
+    prof.disable()
+    print(f"single env: {a.envs * (1 + a.steps) / wall:.1f} env-steps/s "
+          f"({wall / a.envs * 1e3:.3f} ms per episode of reset + {a.steps} steps)", flush=True)
+    for key in ("tottime", "cumulative"):
+        s = io.StringIO()
+        pstats.Stats(prof, stream=s).sort_stats(key).print_stats(30)
+        print(f"==== by {key}\n" + s.getvalue()[:7000], flush=True)
+
+
+if __name__ == "__main__":
+    main()
