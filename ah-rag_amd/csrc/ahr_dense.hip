@@ -3891,15 +3891,15 @@ void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, 
                        ix->dim, normalize_q, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base,
                        k, ix->part, fc, fs, fr, fk);
   };
-  static std::atomic<uint64_t> a12{0}, a42{0};
+  static std::atomic<uint64_t> a12{0}, a10{0}, a42{0}, a40{0};  // per instantiation
   if (B == 1 && slots == 2)
     go(topk_small_f32_kernel<KCAP, 1, 2>, a12);
   else if (B == 1)
-    go(topk_small_f32_kernel<KCAP, 1, 0>, a12);
+    go(topk_small_f32_kernel<KCAP, 1, 0>, a10);
   else if (slots == 2)
     go(topk_small_f32_kernel<KCAP, 4, 2>, a42);
   else
-    go(topk_small_f32_kernel<KCAP, 4, 0>, a42);
+    go(topk_small_f32_kernel<KCAP, 4, 0>, a40);
 }
 
 template <int DT>
