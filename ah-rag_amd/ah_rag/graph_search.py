@@ -177,6 +177,31 @@ class DeviceGraph:
                 nat.ptr(osc), nat.ptr(oc), nat.stream_ptr(stream)), "ahr_graph_expand_rerank")
         return RerankResult(en, es, ex, ec, on, osem, osc, oc, arena)
 
+    def rerank_specs(self, B: int, k: int, params: "RerankParams"):
+        """(shape, dtype) of expand_rerank's eight outputs for B queries of k seeds (_arena order)."""
+        fan = max(2, params.member_top_m)
+        max_exp = max(1, k * (1 + fan))
+        kk = max(max(params.top_k, 0), 1)
+        return [((B, max_exp), torch.int32), ((B, max_exp), torch.float64), ((B, max_exp), torch.int32),
+                ((B,), torch.int32), ((B, kk), torch.int32), ((B, kk), torch.float64), ((B, kk), torch.float64),
+                ((B,), torch.int32)]
+
+    def expand_rerank_rows(self, rows: torch.Tensor, scores: torch.Tensor, row_to_node: torch.Tensor,
+                           params: "RerankParams", outs: Sequence[torch.Tensor], arena: torch.Tensor,
+                           stream: Optional[torch.cuda.Stream] = None) -> "RerankResult":
+        """expand_rerank fed by the dense step's rows directly (ahr_graph_expand_rerank_rows: the
+        row -> node gather inside the kernel); `outs` = views of `arena` shaped by rerank_specs."""
+        B, k = rows.shape
+        max_exp = outs[0].shape[1]
+        c = params.to_c()
+        _on_stream(stream, self.device, rows, scores, row_to_node, arena)
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().ahr_graph_expand_rerank_rows(
+                self._h, nat.ptr(rows), nat.ptr(row_to_node), int(row_to_node.shape[0]), nat.ptr(scores), B, k,
+                nat.ctypes.byref(c), max_exp, *(nat.ptr(t) for t in outs), nat.stream_ptr(stream)),
+                "ahr_graph_expand_rerank_rows")
+        return RerankResult(*outs, arena)
+
     def lca(self, inputs: torch.Tensor, max_out: int = 1024,
             stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Batched expand_to_lca core (ahr_graph_lca): inputs int32 [B, n_in] node indices ->
@@ -294,9 +319,10 @@ _ELEM = {torch.int32: (4, np.int32), torch.float64: (8, np.float64), torch.float
          torch.int64: (8, np.int64), torch.uint8: (1, np.uint8)}
 
 
-def _arena(dev: torch.device, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]]):
+def _arena(dev: torch.device, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]], first: Optional[int] = None):
     """One uninitialised device buffer holding tensors of the given (shape, dtype)s, each at an
-    8-byte aligned offset: (buffer, views)."""
+    8-byte aligned offset: (buffer, views). With `first`, only the first `first` views are made and
+    the third item is a callable that makes the rest (so a launch can go out before them)."""
     offs, sizes, total = [], [], 0
     for shape, dt in specs:
         n = math.prod(shape) * _ELEM[dt][0]
@@ -304,12 +330,17 @@ def _arena(dev: torch.device, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype
         sizes.append(n)
         total += (n + 7) // 8 * 8
     buf = torch.empty(max(total, 8), dtype=torch.uint8, device=dev)
-    views = []
-    for (shape, dt), o, n in zip(specs, offs, sizes):
-        v = buf[o:o + n].view(dt).view(shape)
-        v._ahr_arena = (buf, o)  # (a dtype view is not tracked as a view of buf: to_host_arrays)
-        views.append(v)
-    return buf, views
+
+    def make(i0, i1):
+        views = []
+        for (shape, dt), o, n in zip(specs[i0:i1], offs[i0:i1], sizes[i0:i1]):
+            v = buf[o:o + n].view(dt).view(shape)
+            v._ahr_arena = (buf, o)  # (a dtype view is not tracked as a view of buf: to_host_arrays)
+            views.append(v)
+        return views
+    if first is None:
+        return buf, make(0, len(specs))
+    return buf, make(0, first), lambda: make(first, len(specs))
 
 
 def to_host_arrays(*tensors: torch.Tensor) -> List[np.ndarray]:
@@ -393,14 +424,16 @@ class SearchEngine:
         # rows past the index count come back as -1 anyway: ask for at most count (Chroma's
         # n_results clamp), so a small corpus answers any top_k
         k_dense = min(k, max(1, len(self.index)), nat.AHR_MAX_K_LARGE)
+        B = int(query_vectors.shape[0]) if query_vectors.dim() > 1 else 1
+        # the dense scores / rows and the eight rerank outputs in one device buffer: one host copy
+        arena, (scores, rows), rest = _arena(
+            self.graph.device, [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)]
+            + self.graph.rerank_specs(B, k_dense, params), first=2)
         with devtime.span(None, self.graph.device):  # (recorded on the current stream, after the waits)
-            scores, rows = self.index.query(query_vectors, k_dense, stream=stream)
-            if stream is not None:  # the gather below and the host copies run on the current stream
-                torch.cuda.current_stream(self.graph.device).wait_stream(stream)
-            valid = rows >= 0
-            nodes = torch.where(valid, self.row_to_node[rows.clamp_min(0).long()], torch.full_like(rows, -1))
-            res = self.graph.expand_rerank(nodes, scores, params, stream=stream)
-            if stream is not None:
+            self.index.query(query_vectors, k_dense, stream=stream, out=(scores, rows))
+            res = self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, rest(), arena,
+                                                stream=stream)
+            if stream is not None:  # the host copies run on the current stream
                 torch.cuda.current_stream(self.graph.device).wait_stream(stream)
         host, rows_h, scores_h = res.to_host(rows, scores)
         return rows_h, scores_h, host

@@ -76,7 +76,8 @@ __device__ __forceinline__ bool has_entry(const int32_t* list, int n, int32_t v)
 }
 
 __global__ __launch_bounds__(64) void expand_rerank_kernel(
-    DevGraph g, const int32_t* __restrict__ seed_nodes, const float* __restrict__ seed_sem, int B,
+    DevGraph g, const int32_t* __restrict__ seed_nodes, const int32_t* __restrict__ row_map, int64_t n_map,
+    const float* __restrict__ seed_sem, int B,
     int k_seed, ahr_rerank_params p, int max_exp, int32_t* __restrict__ exp_nodes,
     double* __restrict__ exp_sem, int32_t* __restrict__ exp_src, int32_t* __restrict__ exp_count,
     int32_t* __restrict__ out_nodes, double* __restrict__ out_sem, double* __restrict__ out_score,
@@ -91,7 +92,9 @@ __global__ __launch_bounds__(64) void expand_rerank_kernel(
   // ---- expansion: hierarchical_graph.py:727-740 (dict insertion order; seeds overwrite in
   // place, expansions only add absent ids)
   for (int s = 0; s < k_seed; ++s) {
-    const int32_t nid = seed_nodes[(int64_t)q * k_seed + s];
+    int32_t nid = seed_nodes[(int64_t)q * k_seed + s];
+    if (row_map)  // seed_nodes are dense-index rows: their node indices (-1: no hit)
+      nid = nid >= 0 && nid < n_map ? row_map[nid] : -1;
     if (nid < 0) continue;  // no hit (Chroma returned fewer ids)
     // semantic = 1.0 - float(dist) (:719-724), dist = Chroma's float32 cosine distance 1 - score
     const float dist = 1.0f - seed_sem[(int64_t)q * k_seed + s];
@@ -583,11 +586,11 @@ int ahr_graph_info(const ahr_graph* g, int64_t* n_nodes, int64_t* n_edges) {
   return AHR_OK;
 }
 
-int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float* seed_sem, int B,
-                            int k_seed, const ahr_rerank_params* params, int max_exp,
-                            int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
-                            int32_t* exp_count, int32_t* out_nodes, double* out_sem,
-                            double* out_score, int32_t* out_count, void* stream) {
+static int expand_rerank_impl(ahr_graph* g, const int32_t* seed_nodes, const int32_t* row_map, int64_t n_map,
+                              const float* seed_sem, int B, int k_seed, const ahr_rerank_params* params,
+                              int max_exp, int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
+                              int32_t* exp_count, int32_t* out_nodes, double* out_sem, double* out_score,
+                              int32_t* out_count, void* stream) {
   if (!g || !params) return fail(AHR_EINVAL, "null graph or params");
   if (B < 0 || k_seed < 0 || params->top_k < 0 || params->member_top_m < 0)
     return fail(AHR_EINVAL, "negative size");
@@ -600,11 +603,30 @@ int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float
   const ahr_rerank_params p = *params;
   DeviceGuardG dg(g->device);
   hipLaunchKernelGGL(expand_rerank_kernel, dim3((B + 63) / 64), dim3(64), 0,
-                     reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, seed_sem, B, k_seed,
-                     p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
+                     reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
+                     k_seed, p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
                      out_score, out_count);
   AHR_HIP(hipGetLastError());
   return AHR_OK;
+}
+
+int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float* seed_sem, int B,
+                            int k_seed, const ahr_rerank_params* params, int max_exp,
+                            int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
+                            int32_t* exp_count, int32_t* out_nodes, double* out_sem,
+                            double* out_score, int32_t* out_count, void* stream) {
+  return expand_rerank_impl(g, seed_nodes, nullptr, 0, seed_sem, B, k_seed, params, max_exp, exp_nodes, exp_sem,
+                            exp_src, exp_count, out_nodes, out_sem, out_score, out_count, stream);
+}
+
+int ahr_graph_expand_rerank_rows(ahr_graph* g, const int32_t* rows, const int32_t* row_to_node, int64_t n_rows,
+                                 const float* seed_sem, int B, int k_seed, const ahr_rerank_params* params,
+                                 int max_exp, int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
+                                 int32_t* exp_count, int32_t* out_nodes, double* out_sem, double* out_score,
+                                 int32_t* out_count, void* stream) {
+  if (!row_to_node || n_rows < 0) return fail(AHR_EINVAL, "null row map or negative row count");
+  return expand_rerank_impl(g, rows, row_to_node, n_rows, seed_sem, B, k_seed, params, max_exp, exp_nodes,
+                            exp_sem, exp_src, exp_count, out_nodes, out_sem, out_score, out_count, stream);
 }
 
 int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int n_in, int limit,

@@ -254,6 +254,17 @@ int ahr_graph_expand_rerank(ahr_graph* g, const int32_t* seed_nodes, const float
                             int32_t* exp_count, int32_t* out_nodes, double* out_sem,
                             double* out_score, int32_t* out_count, void* stream);
 
+/* The same, fed straight from ahr_index_query's rows: seed b,s is node row_to_node[rows[b][s]]
+ * (rows[b][s] < 0 or >= n_rows: absent), the search path's row -> node gather folded into the
+ * kernel (hierarchical_graph.py:714-726: Chroma ids -> graph nodes). row_to_node: device int32
+ * [n_rows] (>= n_nodes = id unknown to the graph). */
+int ahr_graph_expand_rerank_rows(ahr_graph* g, const int32_t* rows, const int32_t* row_to_node,
+                                 int64_t n_rows, const float* seed_sem, int B, int k_seed,
+                                 const ahr_rerank_params* params, int max_exp, int32_t* exp_nodes,
+                                 double* exp_sem, int32_t* exp_src, int32_t* exp_count,
+                                 int32_t* out_nodes, double* out_sem, double* out_score,
+                                 int32_t* out_count, void* stream);
+
 /* Batched environment expansions (environment.py:393-480).
  * action: 0 expand_parents, 1 expand_children, 2 expand_related.
  * inputs: device int32 [B][n_in] (-1 = absent / not in graph); out: device int32 [B][limit],

@@ -122,7 +122,7 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
     reset_ms, step_ms = np.mean(reset_wall) * 1e3, float(np.sum([np.mean(w) for w in step_wall])) * 1e3 / steps
     dev_reset, dev_step = float(np.mean(dev_ms["reset"])), float(np.mean(dev_ms["step"]))
 
-    single_rate = None
+    single_rate = search_s = None
     if rank == 0 and single > 0:
         # single-environment loop (B = 1 per search / expansion), a subset of the same queries
         n1 = min(single, envs)
@@ -140,6 +140,16 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
             for _ in range(steps):
                 env.step(random_actions(rng, [env.get_action_mask()])[0])
         single_rate = round(n1 * (1 + steps) / (time.perf_counter() - ts), 1)
+        # the drop-in search itself: HierarchicalGraph.search's body at B = 1 (dense top-5 + expansion
+        # + rerank + the result dicts, return_cluster=False) with a precomputed query vector
+        n_s = min(256, envs)
+        for i in range(8):
+            hg.search_batch([queries[i]], top_k=5, member_top_m=5, query_vectors=qv[i:i + 1])
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for i in range(n_s):
+            hg.search_batch([queries[i]], top_k=5, member_top_m=5, query_vectors=qv[i:i + 1])
+        search_s = (time.perf_counter() - ts) / n_s
     cpu = None
     if rank == 0 and cpu_baseline_fn is not None:
         cpu = cpu_baseline_fn(hg, ids, vectors, qv, steps)
@@ -161,6 +171,11 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
             "how": "device = HIP-event spans around every search / expansion pass (ah_rag.devtime) on the "
                    "launch stream, summed; host = wall - device; means over the timed episodes"},
         "single_env_steps_per_s": single_rate,
+        "dropin_search_b1": None if search_s is None else {
+            "calls_per_s": round(1.0 / search_s, 1), "ms_per_call": round(search_s * 1e3, 4),
+            "what": "HierarchicalGraph.search_batch([q], top_k=5, return_cluster=False) wall time per "
+                    "call at B = 1 with a precomputed query vector (the body of the drop-in search(); "
+                    "fp32 index, 90k rows), 256 calls after 8 warm-up calls"},
         "cpu_baseline": cpu,
         "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
         "build_s": round(t_build, 1), "parallelism": f"replicas{world} (environments partitioned, no collective)",

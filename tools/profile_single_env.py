@@ -3,7 +3,8 @@
 AHRAGGymEnv stepped one environment at a time (tools/bench_env.py's `single` leg: reset at B = 1
 with a precomputed query vector, then random valid actions), profiled over --envs episodes after
 one warm-up episode; prints the wall rate and the top functions by own and cumulative time.
-usage: python tools/profile_single_env.py [--envs 64] [--steps 6]
+usage: python tools/profile_single_env.py [--envs 64] [--steps 6] [--search]
+(--search: profile HierarchicalGraph.search_batch at B = 1, return_cluster=False, instead)
 """
 import argparse
 import cProfile
@@ -29,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=64)
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--search", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(7)
@@ -42,6 +44,9 @@ def main():
     env.env.logging_enabled = False
 
     def episode(i):
+        if a.search:
+            hg.search_batch([f"q{i}"], top_k=5, member_top_m=5, query_vectors=qv[i:i + 1])
+            return
         bench_env.single_reset(env, hg, f"q{i}", qv[i:i + 1])
         for _ in range(a.steps):
             env.step(bench_env.random_actions(rng, [env.get_action_mask()])[0])
@@ -57,8 +62,11 @@ def main():
     for i in range(a.envs):
         episode(i)
     prof.disable()
-    print(f"single env: {a.envs * (1 + a.steps) / wall:.1f} env-steps/s "
-          f"({wall / a.envs * 1e3:.3f} ms per episode of reset + {a.steps} steps)", flush=True)
+    if a.search:
+        print(f"search_batch B = 1: {a.envs / wall:.1f} calls/s ({wall / a.envs * 1e3:.4f} ms per call)", flush=True)
+    else:
+        print(f"single env: {a.envs * (1 + a.steps) / wall:.1f} env-steps/s "
+              f"({wall / a.envs * 1e3:.3f} ms per episode of reset + {a.steps} steps)", flush=True)
     for key in ("tottime", "cumulative"):
         s = io.StringIO()
         pstats.Stats(prof, stream=s).sort_stats(key).print_stats(30)
