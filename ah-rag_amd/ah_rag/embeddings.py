@@ -118,7 +118,7 @@ def _as_f32_device(x: ArrayLike, device: torch.device) -> torch.Tensor:
         t = torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.float32)))
     if t.dim() == 1:
         t = t.unsqueeze(0)
-    if t.device.type == "cpu" and device.type == "cuda" and t.numel() <= (1 << 20):
+    if t.device.type == "cpu" and device.type == "cuda" and t.numel() <= (1 << 16):
         # a small host batch (the drop-in B = 1 search): staged in pinned memory and copied
         # asynchronously on the current stream, not a pageable copy that blocks the caller
         return t.to(torch.float32).contiguous().pin_memory().to(device, non_blocking=True)
