@@ -2616,8 +2616,10 @@ inline int lds_bytes(int64_t row_stride, int kcap, int ng, bool dma = false) {
   const int64_t l = (int64_t)16 * 4 * waves(ng) * kcap * 8;
   return (int)(q > l ? q : l);
 }
-// the DMA form (A/B: AHR_SMALL_DMA=1) where it fits 160 KiB of LDS
+// the DMA form (A/B: AHR_SMALL_DMA=1, the ablation build only: not the default, so not shipped)
+// where it fits 160 KiB of LDS
 inline bool use_dma(int64_t row_stride, int ng) {
+  if (!kAblation) return false;
   static const bool on = [] {
     const char* e = getenv("AHR_SMALL_DMA");
     return e && atoi(e) != 0;
@@ -2851,9 +2853,9 @@ inline int env_int(const char* name, int dflt, int lo, int hi) {
   const char* e = getenv(name);
   return e ? std::max(lo, std::min(hi, atoi(e))) : dflt;
 }
-inline int slots() {
+inline int slots() {  // (the register form, 0, is compiled into the ablation build only)
   static const int v = env_int("AHR_F32_SLOTS", 2, 0, 2);
-  return v == 1 ? 2 : v;
+  return kAblation && v == 0 ? 0 : 2;
 }
 inline int waves_per_split() {
   static const int w = env_int("AHR_F32_WPS", 1, 1, kWaves);
@@ -3847,12 +3849,15 @@ void launch_small(const ahr_index* ix, const SearchPlan& p, const float* q, int 
                        fold ? fold->keys : nullptr);
   };
   static std::atomic<uint64_t> a_reg{0}, a_dma{0};
+#ifdef AHR_ABLATION
   if constexpr (NG == 1) {
     if (dma) {
       go(&topk_small_kernel<DT, KCAP, NG, true>, a_dma);
       return;
     }
   }
+#endif
+  (void)a_dma;
   go(&topk_small_kernel<DT, KCAP, NG, false>, a_reg);
 }
 
@@ -3891,15 +3896,21 @@ void launch_small_f32_k(const ahr_index* ix, const SearchPlan& p, int B, int k, 
                        ix->dim, normalize_q, ix->qbuf, ix->row_stride, (int)ix->count, B, n_lines, p.n_splits, row_base,
                        k, ix->part, fc, fs, fr, fk);
   };
-  static std::atomic<uint64_t> a12{0}, a10{0}, a42{0}, a40{0};  // per instantiation
-  if (B == 1 && slots == 2)
+  static std::atomic<uint64_t> a12{0}, a42{0};  // per instantiation
+#ifdef AHR_ABLATION
+  static std::atomic<uint64_t> a10{0}, a40{0};
+  if (slots == 0) {
+    if (B == 1)
+      go(topk_small_f32_kernel<KCAP, 1, 0>, a10);
+    else
+      go(topk_small_f32_kernel<KCAP, 4, 0>, a40);
+    return;
+  }
+#endif
+  if (B == 1)
     go(topk_small_f32_kernel<KCAP, 1, 2>, a12);
-  else if (B == 1)
-    go(topk_small_f32_kernel<KCAP, 1, 0>, a10);
-  else if (slots == 2)
-    go(topk_small_f32_kernel<KCAP, 4, 2>, a42);
   else
-    go(topk_small_f32_kernel<KCAP, 4, 0>, a40);
+    go(topk_small_f32_kernel<KCAP, 4, 2>, a42);
 }
 
 template <int DT>

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the non-default forms are in the ablation build: copy ah-rag_amd/ah_rag/_lib/ablation to a
+# gpurun-visible directory, e.g. _lib/abl, and export AHR_LIB_PATH=<that>/libahr_hip.so first)
 # fp32 small kernel A/B (B = 1 and 4, C2 corpus): load form AHR_F32_SLOTS (0 = per-lane register
 # loads, 2 = LDS-DMA whole lines) x split count AHR_F32_WPS (1 = 256 workgroups, 8 = ceil(items / 8)),
 # after the fp32 parity tests under each load form. usage: bash tools/gpu/f32_ab.sh gpurun_out/<dir>

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the non-default forms are in the ablation build: copy ah-rag_amd/ah_rag/_lib/ablation to a
+# gpurun-visible directory, e.g. _lib/abl, and export AHR_LIB_PATH=<that>/libahr_hip.so first)
 # bf16 small kernel: register loads vs LDS-DMA items (AHR_SMALL_DMA), parity under the DMA form,
 # kernel stage (serial, warm / cold) and bench lines at B = 1 and 16 (default in-flight count).
 set -o pipefail
