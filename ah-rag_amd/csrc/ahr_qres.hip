@@ -14,8 +14,10 @@
 //
 // * Corpus: 32-row blocks. At d_pad = 768 one 48-KiB stage per block in a 2-slot ring issued a
 //   whole block ahead (two 24-KiB stages per block in a 3-slot ring measured 9 us slower at C2); at
-//   384 one 24-KiB stage per block in a 3-slot ring issued two blocks ahead. Buffer LDS-DMA of 1-KiB pieces (8 whole 128-B rows), the XOR chunk swizzle of
-//   the tile kernels (conflict-free ds_read_b128). One barrier per stage.
+//   384 (round 5) two blocks per 48-KiB stage in a 2-slot ring, one barrier per two blocks (one
+//   24-KiB stage per block in a 3-slot ring: 113-114 vs 108 us at d = 384, same box). Buffer
+//   LDS-DMA of 1-KiB pieces (8 whole 128-B rows), the XOR chunk swizzle of the tile kernels
+//   (conflict-free ds_read_b128). One barrier per stage.
 // * Scores: the k-order, fragment map and accumulation chain of topk_tilelane_kernel (step s of
 //   a row covers k = [16 s, 16 s + 16), lane half fh holding 8 of them; the chain starts from 0),
 //   so every score is bitwise the tile kernel's.
@@ -48,25 +50,29 @@ namespace ahr {
 namespace dense {
 namespace qres {
 
-// NKT 64-deep k-tiles per row (12 at d_pad 768, 6 at 384); a ring stage is one whole 32-row block
-// (48 or 24 KiB). 24-KiB stages run a 3-slot ring issued two blocks ahead, 48-KiB stages a 2-slot
-// ring issued one block ahead.
+// NKT 64-deep k-tiles per row (12 at d_pad 768, 6 at 384); a ring stage is kPB whole 32-row blocks
+// (48 KiB: one block at 768, two at 384; AHR_QRES_PB6=1 builds the round-4 one-block 24-KiB stages,
+// a 3-slot ring issued two blocks ahead), 48-KiB stages a 2-slot ring issued one stage ahead.
 constexpr int kLandBytes = 768;
 
 static_assert(kPark >= 6, "the replay of a parked block never overtakes its unread quads");
 
+#ifndef AHR_QRES_PB6
+#define AHR_QRES_PB6 2  // 32-row blocks per ring stage at d_pad 384 (A/B builds: 1)
+#endif
 template <int NKT>
 struct Cfg {
   static_assert(NKT == 6 || NKT == 12, "d_pad 384 or 768");
-  static constexpr int kSK = NKT;                 // k-tiles per stage (= block)
-  static constexpr int kStage = kSK * kKt;        // 24 or 48 KiB
-  static constexpr int kSlots = kSK == 12 ? 2 : 3;
+  static constexpr int kPB = NKT == 6 ? AHR_QRES_PB6 : 1;  // 32-row blocks per stage
+  static constexpr int kSK = NKT;                 // k-tiles per block row
+  static constexpr int kStage = kPB * kSK * kKt;  // 48 KiB (d 768; d 384 with two blocks) or 24 KiB
+  static constexpr int kSlots = kPB * kSK == 12 ? 2 : 3;
   static constexpr int kAhead = kSlots - 1;       // stages in flight beyond the one multiplied
-  static constexpr int kPieces = kSK * 4;         // 1-KiB DMA pieces per stage (8 rows x 128 B)
+  static constexpr int kPieces = kPB * kSK * 4;   // 1-KiB DMA pieces per stage (8 rows x 128 B)
   static_assert(kPieces % kWaves == 0, "equal DMA share per wave");
   static constexpr int kPPW = kPieces / kWaves;   // pieces per wave per stage
   static constexpr int kNS = NKT * 4;             // k16 steps = query fragments per lane
-  static constexpr int kSS = kSK * 4;             // k16 steps per stage
+  static constexpr int kSS = kSK * 4;             // k16 steps per block
   // LDS: the ring, the lane buffers, the landing zones, the event table
   static constexpr int kOffBuf = kSlots * kStage;
   // the seeding events' landing zone, per wave: 64 published maxima (512 B), 32 seeds (256 B)
@@ -207,7 +213,8 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     b_begin = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n_blocks / n_splits));
     b_end = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n_blocks / n_splits));
   }
-  const int n_st = b_end - b_begin;  // ring stages = blocks
+  const int n_bl = b_end - b_begin;                  // the split's blocks
+  const int n_st = (n_bl + C::kPB - 1) / C::kPB;     // ring stages
   // ABL_TRACE (the profiling build only): thread 0 of each workgroup stamps into the buffer passed
   // as thr_init, 64 u64 per workgroup: [0] s_memrealtime at entry, [1] s_memtime at entry, [2] loop
   // entry, [3 + j] after stage j's sync (j <= 55), [59] first event entered, [60] selection done,
@@ -242,20 +249,28 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // registers the main loop cannot spare)
   const uint32_t blk_bytes = (uint32_t)(kTR * row_stride);
   auto slot_of = [&](int st) __attribute__((always_inline)) { return smem + (st % C::kSlots) * C::kStage; };
+  // (kPB = 2: pieces 0 .. 4 kSK - 1 are the stage's first block, the rest its second, laid out after
+  // it in the slot; a stage with one block left reads zeros for the second: out of the descriptor)
   auto issue = [&](int st) __attribute__((always_inline)) {
-    const int b = b_begin + st;
+    const int b = b_begin + st * C::kPB;
+    const int nbs = C::kPB == 1 ? 1 : min(C::kPB, b_end - b);
     const __amdgpu_buffer_rsrc_t r =
-        tile_rsrc(corpus + (int64_t)b * kTR * row_stride, blk_bytes);
+        tile_rsrc(corpus + (int64_t)b * kTR * row_stride, blk_bytes * (uint32_t)nbs);
     unsigned char* slot = slot_of(st);
     int ln = lane;
     asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int i = 0; i < C::kPPW; ++i) {
-      const int p = wave + kWaves * i;
+      // piece wave + 8 i: block h = 8 i / (4 kSK) of the stage (wave < 8 and 4 kSK a multiple of 8:
+      // a compile-time split of the unrolled pieces)
+      constexpr int kPiecesPerBlock = C::kSK * 4;
+      static_assert(kPiecesPerBlock % kWaves == 0, "a wave's pieces split evenly over the blocks");
+      const int h = (kWaves * i) / kPiecesPerBlock;
+      const int p = wave + kWaves * i - h * kPiecesPerBlock;
       const int row = 8 * (p & 3) + (ln >> 3);
-      const uint32_t src_off =
-          (uint32_t)(row * row_stride) + (p >> 2) * kRowBytes + ((((ln & 7) ^ ((row >> 1) & 7))) << 4);
-      blds16(r, src_off, slot + (p >> 2) * kKt + (p & 3) * 1024);
+      const uint32_t src_off = (uint32_t)((h * kTR + row) * row_stride) + (p >> 2) * kRowBytes +
+                               ((((ln & 7) ^ ((row >> 1) & 7))) << 4);
+      blds16(r, src_off, slot + (h * C::kSK + (p >> 2)) * kKt + (p & 3) * 1024);
     }
   };
 #pragma unroll
@@ -576,20 +591,20 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     a_off[m] = fr * kRowBytes + ((((2 * m + fh) ^ ((fr >> 1) & 7))) << 4);
     asm volatile("" : "+v"(a_off[m]));  // materialized once, here
   }
-  auto frag = [&](int st, int s) __attribute__((always_inline)) {
+  auto frag = [&](int st, int s, int h = 0) __attribute__((always_inline)) {  // h: the stage's block
     if constexpr ((ABL & ABL_NOREAD) != 0) return qf[(s + 5) % C::kNS];  // MFMA + issue only
     const unsigned char* slot = slot_of(st);
-    return *reinterpret_cast<const u32x4*>(slot + (s >> 2) * kKt + a_off[s & 3]);
+    return *reinterpret_cast<const u32x4*>(slot + (h * C::kSK + (s >> 2)) * kKt + a_off[s & 3]);
   };
   static_assert(C::kSS % 3 == 0, "three fragment registers rotate evenly over a stage");
   constexpr bool skip_screen = (ABL & ABL_NOSCREEN) != 0;
   f32x16 acc;
   u32x4 fa[3];
   // a block's kSS k16 steps: step t prefetches step t + 2 and multiplies step t
-  auto stage_mma = [&](int st) __attribute__((always_inline)) {
+  auto stage_mma = [&](int st, int h = 0) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < C::kSS; ++t) {
-      if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2);
+      if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2, h);
       __builtin_amdgcn_sched_barrier(0);
       if (t == 0) {
         f32x16 z = {};
@@ -640,37 +655,81 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 #pragma unroll
     for (int S = 0; S < C::kNS; ++S) asm volatile("" : "+v"(qf[S]));
   }
-#pragma unroll 1
-  for (int j = 1; j <= n_st; ++j) {
-    stage_sync(j, young);
-    young = 0;
-    if (j <= 55) stamp(3 + j);
-    const int bi = j - 1;  // the block that ended with stage j - 1
-    const bool first = ss && j == 2;  // uniform
-    // (at the first event the next stage is issued after it: its bounded polls then wait for their
-    // own reads only, not for a stage in flight)
-    const bool ring = j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2);  // (j >= 1: the prologue issued up to kAhead)
-    if (ring && !(first && live)) issue(j + C::kAhead);
-    if (!live) continue;
-    const bool mma = j < n_st;
-    if (mma) {  // the stage's first fragments: in flight under the screening below
-      fa[0] = frag(j, 0);
-      fa[1] = frag(j, 1);
-    }
-    // block bi's screening, then a seeding event (the first one before block 1's screening, which
-    // then runs with the first seed after block 0's parked scores)
-    if (!first) finish_block(bi);
-    if (ss && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
-    if (ss && bi >= 3 && in_sched((uint32_t)(sched >> 32), bi - 1, 1)) seed_read();
-    if (first) {
-      if (ring) {
-        issue(j + C::kAhead);
-        young = 0;  // the ring's pieces are the youngest now: the next sync waits for everything
+  if constexpr (C::kPB == 1) {
+  #pragma unroll 1
+    for (int j = 1; j <= n_st; ++j) {
+      stage_sync(j, young);
+      young = 0;
+      if (j <= 55) stamp(3 + j);
+      const int bi = j - 1;  // the block that ended with stage j - 1
+      const bool first = ss && j == 2;  // uniform
+      // (at the first event the next stage is issued after it: its bounded polls then wait for their
+      // own reads only, not for a stage in flight)
+      const bool ring = j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2);  // (j >= 1: the prologue issued up to kAhead)
+      if (ring && !(first && live)) issue(j + C::kAhead);
+      if (!live) continue;
+      const bool mma = j < n_st;
+      if (mma) {  // the stage's first fragments: in flight under the screening below
+        fa[0] = frag(j, 0);
+        fa[1] = frag(j, 1);
       }
-      replay(b_begin * kTR);
-      finish_block(bi);
+      // block bi's screening, then a seeding event (the first one before block 1's screening, which
+      // then runs with the first seed after block 0's parked scores)
+      if (!first) finish_block(bi);
+      if (ss && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
+      if (ss && bi >= 3 && in_sched((uint32_t)(sched >> 32), bi - 1, 1)) seed_read();
+      if (first) {
+        if (ring) {
+          issue(j + C::kAhead);
+          young = 0;  // the ring's pieces are the youngest now: the next sync waits for everything
+        }
+        replay(b_begin * kTR);
+        finish_block(bi);
+      }
+      if (mma) stage_mma(j);
     }
-    if (mma) stage_mma(j);
+  } else {
+    // One iteration per block bl: at a stage's first block the stage sync and the ring's next issue,
+    // then block bl - 1's screening and seeding steps, then block bl's chain. (kPB = 2: the second
+    // block of a stage runs without a sync: one barrier per two blocks.)
+  #pragma unroll 1
+    for (int bl = 1; bl <= n_bl; ++bl) {
+      const int j = bl / C::kPB;                            // the stage holding block bl
+      const bool at_stage = C::kPB == 1 || (bl & 1) == 0;   // uniform
+      const int bi = bl - 1;                                // the block whose chain just ended
+      const bool first = ss && bi == 1;                     // uniform
+      bool ring = false;
+      if (at_stage) {
+        stage_sync(j, young);
+        young = 0;
+        if (j <= 55) stamp(3 + j);
+        // (at the first event the next stage is issued after it: its bounded polls then wait for
+        // their own reads only, not for a stage in flight)
+        ring = j + C::kAhead < n_st && !((ABL & ABL_NOLOADS) && j >= 2);  // (the prologue issued up to kAhead)
+        if (ring && !(first && live)) issue(j + C::kAhead);
+      }
+      if (!live) continue;
+      const bool mma = bl < n_bl;
+      const int h = C::kPB == 1 ? 0 : (bl & 1);  // block bl's place in its stage
+      if (mma) {  // the block's first fragments: in flight under the screening below
+        fa[0] = frag(j, 0, h);
+        fa[1] = frag(j, 1, h);
+      }
+      // block bi's screening, then a seeding event (the first one before block 1's screening, which
+      // then runs with the first seed after block 0's parked scores)
+      if (!first) finish_block(bi);
+      if (ss && (first || in_sched((uint32_t)(sched >> 32), bi, 1))) event_site(first);
+      if (ss && bi >= 3 && in_sched((uint32_t)(sched >> 32), bi - 1, 1)) seed_read();
+      if (first) {
+        if (ring) {
+          issue(j + C::kAhead);
+          young = 0;  // the ring's pieces are the youngest now: the next sync waits for everything
+        }
+        replay(b_begin * kTR);
+        finish_block(bi);
+      }
+      if (mma) stage_mma(j, h);
+    }
   }
 
   // this lane's buffered keys at or above its final threshold, sorted (the query registers are dead
