@@ -1,7 +1,7 @@
 """Per-workgroup timeline of one topk_qres_kernel launch (development aid, the ablation build).
 
 Thread 0 of every workgroup stamps s_memrealtime (100 MHz) at entry, at loop entry, after every
-stage sync and around the first seeding event, and s_memtime at entry and exit (kFlagQresTrace,
+stage sync (a stage = one 32-row block at d = 768, two at d = 384) and around the first seeding event, and s_memtime at entry and exit (kFlagQresTrace,
 ahr_qres.hip ABL_TRACE). Prints the launch skew, the per-block interval profile over the split
 (median / p90 over workgroups), the first event's parts and the shader clock.
 
@@ -62,7 +62,9 @@ def main():
         t = trace.view(grid, 64).cpu().numpy().astype(np.int64)
         t0 = t[:, 0].min()
         us = lambda x: (x - t0) * TICK_US  # noqa: E731
-        n_st = plan["tiles_per_split"]
+        # ring stages: a stage holds two blocks at d = 384 (kPB = 2), one at 768
+        pb = 2 if a.workload == "hotpot90k_d384" else 1
+        n_st = (plan["tiles_per_split"] + pb - 1) // pb
         js = min(n_st, 55)
         stage = t[:, 3:3 + js + 1]
         d = np.diff(stage, axis=1) * TICK_US  # interval j-1 -> j: block j-1's MMA + block j-2's screening (SPB 1)
