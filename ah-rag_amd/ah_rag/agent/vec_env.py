@@ -353,15 +353,19 @@ class VecAHRAGGymEnv:
         pos = np.arange(K_NODES)[None, :]
         top_valid = pos < prev.sel_n[:, None]
 
-        # expansions (environment.py:393-480): one ahr_graph_expand launch per action kind
+        # expansions (environment.py:393-480): one ahr_graph_expand launch per action kind, all
+        # enqueued before one host copy (one stream sync per step, not one per kind)
+        launched = []
         for act, name in EXPAND_ACTIONS.items():
             g = np.flatnonzero(a == act)
             if not len(g):
                 continue
             t = TOP_IDS[act]
             inp = np.where(top_valid[g, :t] & (prev.sel[g, :t] < n_graph), prev.sel[g, :t], -1)
-            out, cnt = self._engine.graph.expand(name, torch.from_numpy(inp.astype(np.int32)), K_NODES)
-            out_h, cnt_h = (a.astype(np.int64) for a in to_host_arrays(out, cnt))
+            launched.append((g, *self._engine.graph.expand(name, torch.from_numpy(inp.astype(np.int32)), K_NODES)))
+        host = to_host_arrays(*[x for _, out, cnt in launched for x in (out, cnt)])
+        for i, (g, _, _) in enumerate(launched):
+            out_h, cnt_h = host[2 * i].astype(np.int64), host[2 * i + 1].astype(np.int64)
             self._steps[g] += 1
             ob.kind[g] = OBS_EXPAND
             ob.step[g] = self._steps[g]
