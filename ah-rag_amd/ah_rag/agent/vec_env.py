@@ -87,7 +87,13 @@ class _ObsBatch:
         self.cache: Dict[int, Dict[str, Any]] = {}
         self.search = None  # reset: (engine, params, rows, scores, res, seed_idx, seed_sem, seed_n)
 
-    def copy_rows(self, src: "_ObsBatch", idx: np.ndarray) -> None:
+    def copy_rows(self, src: "_ObsBatch", idx: Optional[np.ndarray] = None) -> None:
+        """src's rows idx into this batch (idx None: every row)."""
+        if idx is None:
+            for name in ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size"):
+                getattr(self, name)[:] = getattr(src, name)
+            self.S, self.F = list(src.S), list(src.F)
+            return
         for name in ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size"):
             getattr(self, name)[idx] = getattr(src, name)[idx]
         for e in idx.tolist():
@@ -347,7 +353,7 @@ class VecAHRAGGymEnv:
         self._cur += 1
         n_graph = self._engine.graph.n_nodes
         ob = _ObsBatch(E)
-        ob.copy_rows(prev, np.arange(E))  # the defaults: unchanged (aliased) observations
+        ob.copy_rows(prev)  # the defaults: unchanged (aliased) observations
         ob.alias = [None] * E
         ob.search = prev.search
         pos = np.arange(K_NODES)[None, :]
