@@ -338,7 +338,8 @@ class DenseIndex:
         query-resident kernels, 4096 = the 128-query-resident (qkv) kernel wherever it applies (the
         ablation build only), 16384 = tilelane without the cross-tile prefetch, 32768 = the 256x256
         16x16x32 kernel (bf16/f16, k <= 16), 131072 / 262144 = always / never the k-blocked kernel,
-        1 << 22 = small batches through a merge launch instead of the last-workgroup fold,
+        8192 = small batches (B <= 4) merged by the kernel's last workgroup (the fold) instead of
+        the merge launch (the default), 1 << 22 = the merge launch even with 8192,
         1 << 23 = the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768,
         k <= 12), 1 << 26 = that kernel seeded by the sampled pre-pass instead of seeding itself, 1 << 27 = its
         self-seeding with the first event only, 1 << 28 / 1 << 19 = its splits XCD-balanced at any corpus

@@ -4175,9 +4175,12 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   }
   // single searches (the drop-in's search() and environment resets): the small kernels merge the
   // splits in their last workgroup, no merge launch
+  // The last-workgroup fold is opt-in (kFlagFold): the merge launch measured faster from round 5
+  // (fp32 B = 1 two in flight 25.2-25.7 k vs 21.6-22.0 k queries/s, bf16 41.9-42.0 k vs 36.9-37.3 k,
+  // serial equal: the next batch's stream overlaps the merge, while the fold's tail holds the kernel)
   const bool fold = ix->count > 0 && p.kernel == KERNEL_SMALL && B <= kFoldMaxQ &&
                     (int64_t)B * p.n_splits * k * 8 + 16 <= kFoldMaxLds && p.n_splits <= 512 &&
-                    !(ix->debug_flags & kFlagNoFold);
+                    (ix->debug_flags & kFlagFold) && !(ix->debug_flags & kFlagNoFold);
   const FoldOut fo{ix->fold_ctr(), scores, rows, keys};
   if (ix->count > 0) {
     switch (ix->dtype) {

@@ -252,7 +252,8 @@ enum : uint32_t {
   kFlagNoKB256 = 262144,  // plan without the k-blocked kernel
   kFlagTileZero = 1u << 20,   // k-blocked kernel: every tile's operands read from tile 0 (L2-resident; wrong results)
   kFlagTileFirst = 1u << 21,  // k-blocked kernel: every tile read from the split's first tile (wrong results)
-  kFlagNoFold = 1u << 22,     // small kernels: merge launch instead of the last-workgroup fold (A/B)
+  kFlagNoFold = 1u << 22,     // small kernels: merge launch (the default since round 5; kept accepted)
+  kFlagFold = 8192,           // small kernels: the last-workgroup fold instead of the merge launch (A/B)
   kFlagQres = 1u << 23,       // the 256-query register-resident kernel wherever it applies (bf16/f16, d 384/768, k <= 12)
   kFlagNoBarrier = 1u << 24,  // qres kernel: no stage barriers (wrong results)
   kFlagNoLdsRead = 1u << 25,  // qres kernel: MFMAs on a register fragment, no LDS reads (wrong results)
@@ -282,7 +283,7 @@ constexpr uint32_t kWrongResultFlags = kFlagSkipEpilogue | kFlagMaxOnly | kFlagN
                                        kFlagQresEvNoSel | kFlagQresEvNoIssue;
 // (the 128-query-resident kernel, kFlagQkv, is compiled into the ablation build only)
 constexpr uint32_t kKnownFlags = (kKernelFlags & (kAblation ? ~0u : ~(uint32_t)kFlagQkv)) | kWrongResultFlags |
-                                 kFlagNoTilePrefetch | kFlagNoFold | kFlagQresPrepass | kFlagQresSeedOnce |
+                                 kFlagNoTilePrefetch | kFlagNoFold | kFlagFold | kFlagQresPrepass | kFlagQresSeedOnce |
                                  kFlagXcdBalance | kFlagNoXcdBalance | kFlagQresMute;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 

@@ -130,8 +130,9 @@ int ahr_index_probe_seed(ahr_index* ix, const float* q, int B, int k, int normal
  * screening, 32 = the 128x128 lane-local tile kernel at any batch (k <= 16), 2048 = no
  * query-resident kernel (qkv or qres256), 16384 = tilelane without the cross-tile prefetch, 32768 =
  * the 256x256 16x16x32 kernel, 131072 = the k-blocked 256x256 kernel wherever it applies, 262144 =
- * never the k-blocked kernel, 1 << 19 = qres256 splits never XCD-balanced, 1 << 22 = small batches
- * merge through a merge launch instead of the last-workgroup fold, 1 << 23 = the 256-query
+ * never the k-blocked kernel, 1 << 19 = qres256 splits never XCD-balanced, 8192 = small batches
+ * (B <= 4) merge in the kernel's last workgroup (the fold) instead of the merge launch (the default
+ * since round 5), 1 << 22 = the merge launch even with 8192 set, 1 << 23 = the 256-query
  * register-resident kernel (qres256) wherever it applies (bf16/f16, d_pad 384 or 768, k <= 12),
  * 1 << 26 = qres256 seeded by the sampled pre-pass launch instead of seeding itself, 1 << 27 =
  * qres256's self-seeding with its first event only (no later rounds), 1 << 28 = qres256 splits

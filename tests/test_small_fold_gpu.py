@@ -1,5 +1,5 @@
-"""Small-batch fold: at B <= 4 the small kernels' last-arriving workgroup merges the per-split lists
-(no merge launch). Results must equal the merge-launch path (flag 1 << 22) bit for bit, for every
+"""Small-batch fold (opt-in, flag 8192): at B <= 4 the small kernels' last-arriving workgroup merges
+the per-split lists (no merge launch). Results must equal the merge-launch path (the default) bit for bit, for every
 storage type, ties across splits, k > n, ragged splits, back-to-back calls (the arrival counter
 resets itself), the keyed query and two workspaces on two streams.
 """
@@ -11,7 +11,7 @@ from oracle import dense_ref as dr
 
 pytestmark = pytest.mark.gpu
 
-NO_FOLD = 1 << 22
+FOLD = 8192  # the fold is opt-in (the merge launch measured faster from round 5)
 
 
 def _clustered(rng, n, d, n_centers=64, noise=0.35):
@@ -21,11 +21,10 @@ def _clustered(rng, n, d, n_centers=64, noise=0.35):
 
 
 def _pair(ix, Q, k, **kw):
-    ix.set_debug_flags(0)
+    ix.set_debug_flags(FOLD)
     a = [t.cpu().numpy() for t in ix.query(Q, k, **kw)]
-    ix.set_debug_flags(NO_FOLD)
-    b = [t.cpu().numpy() for t in ix.query(Q, k, **kw)]
     ix.set_debug_flags(0)
+    b = [t.cpu().numpy() for t in ix.query(Q, k, **kw)]
     return a, b
 
 
@@ -61,9 +60,10 @@ def test_fold_ties_repeats_keys(cuda):
     ix.upsert(C)
     Qs = [_clustered(rng, 1 + (i % 4), 768) for i in range(50)]
     ks = [1 + (i * 7) % 16 for i in range(50)]
+    ix.set_debug_flags(FOLD)
     got = [[t.cpu().numpy() for t in ix.query(q, k)] for q, k in zip(Qs, ks)]
     keys = ix.query_keys(Qs[3], 10, row_base=1234).cpu().numpy()
-    ix.set_debug_flags(NO_FOLD)
+    ix.set_debug_flags(0)
     ref = [[t.cpu().numpy() for t in ix.query(q, k)] for q, k in zip(Qs, ks)]
     keys_ref = ix.query_keys(Qs[3], 10, row_base=1234).cpu().numpy()
     ix.close()
@@ -87,6 +87,7 @@ def test_fold_two_streams(cuda):
     C = _clustered(rng, 60000, 768)
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
+    ix.set_debug_flags(FOLD)
     Qs = [torch.from_numpy(_clustered(rng, 1 + i % 4, 768)).to(cuda) for i in range(16)]
     serial = [[t.cpu().numpy() for t in ix.query(q, 10)] for q in Qs]
     for i in range(2):
@@ -119,6 +120,7 @@ def test_fold_empty_split_lists(cuda, dtype):
         C = _clustered(rng, n, 768)
         ix = DenseIndex(768, n, dtype=dtype, device=cuda)
         ix.upsert(C)
+        ix.set_debug_flags(FOLD)
         Cs = dr.round_to_storage(C, dtype) if dtype != "f32" else C
         for it in range(60):
             B = 2 + it % 3

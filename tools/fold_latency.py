@@ -2,7 +2,7 @@
 
 Per storage type and batch (1, 4): wall time per call of back-to-back serial queries (one stream,
 synchronised at the end), and of two batches in flight (two streams / workspaces), for the fold
-(default) and the merge launch (flag 1 << 22), interleaved over rounds; best round reported.
+(opt-in flag 8192) and the merge launch (the default), interleaved over rounds; best round reported.
 """
 import argparse
 import json
@@ -18,7 +18,7 @@ import torch  # noqa: E402
 from ah_rag.embeddings import DenseIndex  # noqa: E402
 from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus  # noqa: E402
 
-NO_FOLD = 1 << 22
+FOLD = 8192
 
 
 def timed(ix, q, k, calls, streams):
@@ -57,7 +57,7 @@ def main():
             q, _ = c.queries(B, rows)
             res = {}
             for _ in range(a.rounds):
-                for name, flags in (("fold", 0), ("merge_launch", NO_FOLD)):
+                for name, flags in (("fold", FOLD), ("merge_launch", 0)):
                     ix.set_debug_flags(flags)
                     res.setdefault(name + "_serial_us", []).append(timed(ix, q, 10, a.calls, s2[:1]))
                     res.setdefault(name + "_inflight2_us", []).append(timed(ix, q, 10, a.calls, s2))
