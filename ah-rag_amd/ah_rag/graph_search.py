@@ -187,20 +187,20 @@ class DeviceGraph:
                 ((B,), torch.int32)]
 
     def expand_rerank_rows(self, rows: torch.Tensor, scores: torch.Tensor, row_to_node: torch.Tensor,
-                           params: "RerankParams", outs: Sequence[torch.Tensor], arena: torch.Tensor,
-                           stream: Optional[torch.cuda.Stream] = None) -> "RerankResult":
+                           params: "RerankParams", max_exp: int, out_ptrs: Sequence[int], arena: torch.Tensor,
+                           stream: Optional[torch.cuda.Stream] = None) -> None:
         """expand_rerank fed by the dense step's rows directly (ahr_graph_expand_rerank_rows: the
-        row -> node gather inside the kernel); `outs` = views of `arena` shaped by rerank_specs."""
+        row -> node gather inside the kernel); `out_ptrs` = device addresses of the eight outputs
+        inside `arena`, laid out by rerank_specs (no tensor views: the caller reads them on the
+        host only)."""
         B, k = rows.shape
-        max_exp = outs[0].shape[1]
         c = params.to_c()
         _on_stream(stream, self.device, rows, scores, row_to_node, arena)
         with torch.cuda.device(self.device):
             nat.check(nat.lib().ahr_graph_expand_rerank_rows(
                 self._h, nat.ptr(rows), nat.ptr(row_to_node), int(row_to_node.shape[0]), nat.ptr(scores), B, k,
-                nat.ctypes.byref(c), max_exp, *(nat.ptr(t) for t in outs), nat.stream_ptr(stream)),
+                nat.ctypes.byref(c), int(max_exp), *out_ptrs, nat.stream_ptr(stream)),
                 "ahr_graph_expand_rerank_rows")
-        return RerankResult(*outs, arena)
 
     def lca(self, inputs: torch.Tensor, max_out: int = 1024,
             stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -319,28 +319,38 @@ _ELEM = {torch.int32: (4, np.int32), torch.float64: (8, np.float64), torch.float
          torch.int64: (8, np.int64), torch.uint8: (1, np.uint8)}
 
 
-def _arena(dev: torch.device, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]], first: Optional[int] = None):
-    """One uninitialised device buffer holding tensors of the given (shape, dtype)s, each at an
-    8-byte aligned offset: (buffer, views). With `first`, only the first `first` views are made and
-    the third item is a callable that makes the rest (so a launch can go out before them)."""
-    offs, sizes, total = [], [], 0
+def _layout(specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]]) -> Tuple[List[int], int]:
+    """8-byte aligned offsets of tensors of the given (shape, dtype)s in one buffer, and its size."""
+    offs, total = [], 0
     for shape, dt in specs:
-        n = math.prod(shape) * _ELEM[dt][0]
         offs.append(total)
-        sizes.append(n)
-        total += (n + 7) // 8 * 8
-    buf = torch.empty(max(total, 8), dtype=torch.uint8, device=dev)
+        total += (math.prod(shape) * _ELEM[dt][0] + 7) // 8 * 8
+    return offs, max(total, 8)
 
-    def make(i0, i1):
-        views = []
-        for (shape, dt), o, n in zip(specs[i0:i1], offs[i0:i1], sizes[i0:i1]):
-            v = buf[o:o + n].view(dt).view(shape)
-            v._ahr_arena = (buf, o)  # (a dtype view is not tracked as a view of buf: to_host_arrays)
-            views.append(v)
-        return views
-    if first is None:
-        return buf, make(0, len(specs))
-    return buf, make(0, first), lambda: make(first, len(specs))
+
+def _arena(dev: torch.device, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]], first: Optional[int] = None):
+    """One uninitialised device buffer holding tensors of the given (shape, dtype)s (_layout):
+    (buffer, views). With `first`, views of the first `first` only, and the offsets of all:
+    (buffer, views, offsets) — the rest are passed to a kernel as addresses and read back with
+    _host_views (a tensor view costs a few torch dispatches each)."""
+    offs, total = _layout(specs)
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    views = []
+    for (shape, dt), o in zip(specs[:first], offs):
+        v = buf[o:o + math.prod(shape) * _ELEM[dt][0]].view(dt).view(shape)
+        v._ahr_arena = (buf, o)  # (a dtype view is not tracked as a view of buf: to_host_arrays)
+        views.append(v)
+    return (buf, views) if first is None else (buf, views, offs)
+
+
+def _host_views(host: np.ndarray, specs: Sequence[Tuple[Tuple[int, ...], torch.dtype]],
+                offs: Sequence[int]) -> List[np.ndarray]:
+    """numpy views of a host copy (uint8) of an _arena buffer, one per spec."""
+    out = []
+    for (shape, dt), o in zip(specs, offs):
+        esz, npt = _ELEM[dt]
+        out.append(host[o:o + math.prod(shape) * esz].view(npt).reshape(shape))
+    return out
 
 
 def to_host_arrays(*tensors: torch.Tensor) -> List[np.ndarray]:
@@ -426,14 +436,18 @@ class SearchEngine:
         k_dense = min(k, max(1, len(self.index)), nat.AHR_MAX_K_LARGE)
         B = int(query_vectors.shape[0]) if query_vectors.dim() > 1 else 1
         # the dense scores / rows and the eight rerank outputs in one device buffer: one host copy
-        arena, (scores, rows), rest = _arena(
-            self.graph.device, [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)]
-            + self.graph.rerank_specs(B, k_dense, params), first=2)
-        with devtime.span(None, self.graph.device):  # (recorded on the current stream, after the waits)
+        dev = self.graph.device
+        specs = [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)] + self.graph.rerank_specs(
+            B, k_dense, params)
+        arena, (scores, rows), offs = _arena(dev, specs, first=2)
+        base = arena.data_ptr()
+        with devtime.span(None, dev):  # (recorded on the current stream, after the waits)
             self.index.query(query_vectors, k_dense, stream=stream, out=(scores, rows))
-            res = self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, rest(), arena,
-                                                stream=stream)
-            if stream is not None:  # the host copies run on the current stream
-                torch.cuda.current_stream(self.graph.device).wait_stream(stream)
-        host, rows_h, scores_h = res.to_host(rows, scores)
+            self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, specs[2][0][1],
+                                          [base + o for o in offs[2:]], arena, stream=stream)
+            if stream is not None:  # the host copy runs on the current stream
+                torch.cuda.current_stream(dev).wait_stream(stream)
+        (host_buf,) = to_host_arrays(arena)
+        scores_h, rows_h, *outs = _host_views(host_buf, specs, offs)
+        host = RerankResult(*outs)
         return rows_h, scores_h, host
