@@ -35,6 +35,7 @@
 #include "ahr_qres.h"
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 #include <math.h>
 #include <vector>
@@ -3364,12 +3365,14 @@ struct ahr_index {
   std::vector<hipEvent_t> prof_events;
   int prof_max_calls = 0;
   // The register-resident kernel fills every CU and its first seeding event waits (bounded) for
-  // every split: a batch of this plan on one workspace's stream starts after the previous one's
-  // merge on another (its completion event), so no workgroup of another batch delays its start.
+  // every split: a batch's kernel of this plan on one workspace's stream starts after the previous
+  // one's kernel on another (its completion event; AHR_QRES_CHAIN=merge: after its merge), so no
+  // workgroup of another batch delays its start.
   // The event is recorded only once batches of this plan have come on two streams (qres_multi): on
   // one stream the order is the stream's own, and the record after the merge cost the serial C2
   // step 4.7 us (merge stage 14.0 vs 9.3 us, profiles/r04/ab_endphase). (Two batches in flight
-  // gain nothing over one: bench.py runs this plan with one.)
+  // lose to one: 0.164-0.168 vs 0.153 ms per C2 step, the cross-stream wait costs more than the
+  // overlap saves, profiles/r05/negative/chain_ab; bench.py runs this plan with one.)
   hipEvent_t qres_done = nullptr;
   hipStream_t qres_stream = nullptr;
   bool qres_multi = false;
@@ -3380,6 +3383,35 @@ struct ahr_index {
 namespace {
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Register-resident batches of different streams (ahr_index::qres_done): a batch of this plan waits
+// for the previous one of another stream, so its first seeding event finds every split resident.
+// AHR_QRES_CHAIN=merge orders the whole batches (the conversion waits for the other batch's merge);
+// =kernel only the kernels (the wait right before the launch, the record right after it).
+inline bool qres_chain_at_kernel() {
+  static const bool at_kernel = [] {
+    const char* e = getenv("AHR_QRES_CHAIN");
+    return !(e && strcmp(e, "merge") == 0);
+  }();
+  return at_kernel;
+}
+inline void qres_chain_wait(ahr_index* ix, hipStream_t s) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cap);
+  if (cap == hipStreamCaptureStatusNone && ix->qres_stream && ix->qres_stream != s) {
+    if (ix->qres_multi) (void)hipStreamWaitEvent(s, ix->qres_done, 0);
+    ix->qres_multi = true;  // from the next batch on (this one's predecessor recorded nothing)
+  }
+}
+inline void qres_chain_record(ahr_index* ix, hipStream_t s) {
+  if (!ix->qres_done) return;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cap);
+  if (cap == hipStreamCaptureStatusNone) {
+    if (ix->qres_multi) (void)hipEventRecord(ix->qres_done, s);
+    ix->qres_stream = s;
+  }
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -3967,9 +3999,13 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       const bool once = (flags & kFlagQresSeedOnce) != 0;
       // (<= 64 splits: the lane-list merge follows, which stops at a list's first empty slot)
       const uint32_t qflags = flags | (p.n_splits <= 64 ? kFlagShortLists : 0u);
+      // (AHR_QRES_CHAIN=kernel: only the kernels of two streams' batches are ordered, so one batch's
+      // merge and the next one's query conversion overlap the other's kernel)
+      if (qres_chain_at_kernel()) qres_chain_wait(ix, s);
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
                    p.n_splits, p.qblocks, (int)qflags, self_seed ? ix->ss + kQresTagOff + 1 : nullptr, once ? 1 : sch.pub,
                    once ? 0 : sch.ev, s);
+      if (qres_chain_at_kernel()) qres_chain_record(ix, s);
       return;
     }
     if (p.kernel == KERNEL_KB256) {
@@ -4116,12 +4152,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   if (pre_kernel == KERNEL_QRES) {
     if ((st = ensure_qbuf_kb(ix, s)) || (st = ensure_ss(ix, s))) return st;
     // the whole batch after the previous register-resident batch of another stream (ahr_index::qres_done)
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(s, &cap);
-    if (cap == hipStreamCaptureStatusNone && ix->qres_stream && ix->qres_stream != s) {
-      if (ix->qres_multi) AHR_HIP(hipStreamWaitEvent(s, ix->qres_done, 0));
-      ix->qres_multi = true;  // from the next batch on (this one's predecessor recorded nothing)
-    }
+    if (!qres_chain_at_kernel()) qres_chain_wait(ix, s);
     if (small_fuses_convert(ix) && !normalize_q && qres_self_seeded(ix, plan_search(ix, B, k), k)) {
       // only the fragment-major copy: the self-seeded launch reads nothing else
       const int64_t n16 = cdiv(B, 32) * (ix->d_pad / 16) * 64;
@@ -4199,14 +4230,8 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
                       p.n_splits;
     launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
   }
-  if (p.kernel == KERNEL_QRES && ix->qres_done) {  // the next register-resident launch waits for this batch's merge
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(s, &cap);
-    if (cap == hipStreamCaptureStatusNone) {
-      if (ix->qres_multi) AHR_HIP(hipEventRecord(ix->qres_done, s));
-      ix->qres_stream = s;
-    }
-  }
+  // the next register-resident launch of another stream waits for this batch's merge
+  if (p.kernel == KERNEL_QRES && !qres_chain_at_kernel()) qres_chain_record(ix, s);
   prof_mark(ix, 4, s);
   if (ix->prof_calls < ix->prof_max_calls) ++ix->prof_calls;
   AHR_HIP(hipGetLastError());
