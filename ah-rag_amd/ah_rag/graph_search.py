@@ -443,7 +443,8 @@ class SearchEngine:
         base = arena.data_ptr()
         with devtime.span(None, dev):  # (recorded on the current stream, after the waits)
             self.index.query(query_vectors, k_dense, stream=stream, out=(scores, rows))
-            self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, specs[2][0][1],
+            max_exp = specs[2][0][1]  # rerank_specs: exp_nodes is [B, max_exp]
+            self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, max_exp,
                                           [base + o for o in offs[2:]], arena, stream=stream)
             if stream is not None:  # the host copy runs on the current stream
                 torch.cuda.current_stream(dev).wait_stream(stream)

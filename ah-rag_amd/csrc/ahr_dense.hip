@@ -3371,8 +3371,8 @@ struct ahr_index {
   // The event is recorded only once batches of this plan have come on two streams (qres_multi): on
   // one stream the order is the stream's own, and the record after the merge cost the serial C2
   // step 4.7 us (merge stage 14.0 vs 9.3 us, profiles/r04/ab_endphase). (Two batches in flight
-  // lose to one: 0.164-0.168 vs 0.153 ms per C2 step, the cross-stream wait costs more than the
-  // overlap saves, profiles/r05/negative/chain_ab; bench.py runs this plan with one.)
+  // lose to one: 0.154-0.168 vs 0.152-0.153 ms per C2 step, the kernel runs ~5 us slower beside
+  // the other batch's merge, profiles/r05/negative/chain_ab; bench.py runs this plan with one.)
   hipEvent_t qres_done = nullptr;
   hipStream_t qres_stream = nullptr;
   bool qres_multi = false;
@@ -3395,22 +3395,24 @@ inline bool qres_chain_at_kernel() {
   }();
   return at_kernel;
 }
-inline void qres_chain_wait(ahr_index* ix, hipStream_t s) {
+inline int qres_chain_wait(ahr_index* ix, hipStream_t s) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(s, &cap);
   if (cap == hipStreamCaptureStatusNone && ix->qres_stream && ix->qres_stream != s) {
-    if (ix->qres_multi) (void)hipStreamWaitEvent(s, ix->qres_done, 0);
+    if (ix->qres_multi) AHR_HIP(hipStreamWaitEvent(s, ix->qres_done, 0));
     ix->qres_multi = true;  // from the next batch on (this one's predecessor recorded nothing)
   }
+  return AHR_OK;
 }
-inline void qres_chain_record(ahr_index* ix, hipStream_t s) {
-  if (!ix->qres_done) return;
+inline int qres_chain_record(ahr_index* ix, hipStream_t s) {
+  if (!ix->qres_done) return AHR_OK;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(s, &cap);
   if (cap == hipStreamCaptureStatusNone) {
-    if (ix->qres_multi) (void)hipEventRecord(ix->qres_done, s);
+    if (ix->qres_multi) AHR_HIP(hipEventRecord(ix->qres_done, s));
     ix->qres_stream = s;
   }
+  return AHR_OK;
 }
 
 struct DeviceGuard {
@@ -3999,13 +4001,9 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
       const bool once = (flags & kFlagQresSeedOnce) != 0;
       // (<= 64 splits: the lane-list merge follows, which stops at a list's first empty slot)
       const uint32_t qflags = flags | (p.n_splits <= 64 ? kFlagShortLists : 0u);
-      // (AHR_QRES_CHAIN=kernel: only the kernels of two streams' batches are ordered, so one batch's
-      // merge and the next one's query conversion overlap the other's kernel)
-      if (qres_chain_at_kernel()) qres_chain_wait(ix, s);
       qres::launch(DT, k, ix->rows, ix->qbuf_kb, ix->row_stride, ix->d_pad * ix->elem, n, B, row_base, ix->part, thr,
                    p.n_splits, p.qblocks, (int)qflags, self_seed ? ix->ss + kQresTagOff + 1 : nullptr, once ? 1 : sch.pub,
                    once ? 0 : sch.ev, s);
-      if (qres_chain_at_kernel()) qres_chain_record(ix, s);
       return;
     }
     if (p.kernel == KERNEL_KB256) {
@@ -4152,7 +4150,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
   if (pre_kernel == KERNEL_QRES) {
     if ((st = ensure_qbuf_kb(ix, s)) || (st = ensure_ss(ix, s))) return st;
     // the whole batch after the previous register-resident batch of another stream (ahr_index::qres_done)
-    if (!qres_chain_at_kernel()) qres_chain_wait(ix, s);
+    if (!qres_chain_at_kernel() && (st = qres_chain_wait(ix, s))) return st;
     if (small_fuses_convert(ix) && !normalize_q && qres_self_seeded(ix, plan_search(ix, B, k), k)) {
       // only the fragment-major copy: the self-seeded launch reads nothing else
       const int64_t n16 = cdiv(B, 32) * (ix->d_pad / 16) * 64;
@@ -4213,6 +4211,10 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
                     (int64_t)B * p.n_splits * k * 8 + 16 <= kFoldMaxLds && p.n_splits <= 512 &&
                     (ix->debug_flags & kFlagFold) && !(ix->debug_flags & kFlagNoFold);
   const FoldOut fo{ix->fold_ctr(), scores, rows, keys};
+  // (AHR_QRES_CHAIN=kernel: only the kernels of two streams' register-resident batches are ordered,
+  // so one batch's merge and the next one's query conversion overlap the other's kernel)
+  const bool chain_k = p.kernel == KERNEL_QRES && qres_chain_at_kernel();
+  if (chain_k && (st = qres_chain_wait(ix, s))) return st;
   if (ix->count > 0) {
     switch (ix->dtype) {
       case AHR_BF16: launch_search<DT_BF16>(ix, p, B, k, (uint32_t)row_base, q, normalize_q, fold ? &fo : nullptr, s); break;
@@ -4223,6 +4225,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     prof_mark(ix, 1, s);
     prof_mark(ix, 2, s);
   }
+  if (chain_k && (st = qres_chain_record(ix, s))) return st;
   prof_mark(ix, 3, s);
   if (!fold) {
     // qkv: one list per (split, dimension half); t256 / kb256: one per (split, row half)
@@ -4231,7 +4234,7 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
   }
   // the next register-resident launch of another stream waits for this batch's merge
-  if (p.kernel == KERNEL_QRES && !qres_chain_at_kernel()) qres_chain_record(ix, s);
+  if (p.kernel == KERNEL_QRES && !qres_chain_at_kernel() && (st = qres_chain_record(ix, s))) return st;
   prof_mark(ix, 4, s);
   if (ix->prof_calls < ix->prof_max_calls) ++ix->prof_calls;
   AHR_HIP(hipGetLastError());
