@@ -374,6 +374,5 @@ def expand_batch(hg: HierarchicalGraph, action: str, inputs: Sequence[Sequence[s
     for b, ids in enumerate(inputs):
         if ids:
             idx[b, :len(ids)] = dg.node_indices(ids)
-    out, cnt = dg.expand(action, torch.from_numpy(idx), limit)
-    out_h, cnt_h = to_host_arrays(out, cnt)
+    out_h, cnt_h = dg.expand_host(action, idx, limit)
     return [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] for b in range(len(inputs))]

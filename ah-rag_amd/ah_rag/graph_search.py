@@ -87,6 +87,7 @@ class DeviceGraph:
 
     def __init__(self, G: nx.DiGraph, device: Optional[torch.device] = None) -> None:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self._xbufs: Dict[Tuple[int, int, int], Tuple] = {}  # expand_host's buffers per shape
         self.serial = next(_GRAPH_SERIALS)
         self.ids: List[str] = list(G.nodes)
         self.index: Dict[str, int] = {nid: i for i, nid in enumerate(self.ids)}
@@ -261,6 +262,37 @@ class DeviceGraph:
                       "ahr_graph_expand")
         return out, cnt
 
+    def expand_host(self, action: str, idx: np.ndarray, limit: int = 10) -> Tuple[np.ndarray, np.ndarray]:
+        """expand() of host node indices (int32 [B, n_in], -1 = skip) with host results (out
+        [B, max(limit, 1)], count [B]): the inputs staged in pinned memory and both outputs read
+        back in one copy, with buffers kept per shape and reused (one caller at a time: the
+        single-environment step), one stream sync."""
+        B, n_in = idx.shape
+        lim = max(limit, 1)
+        key = (B, n_in, lim)
+        b = self._xbufs.get(key)
+        if b is None:
+            if len(self._xbufs) >= 8:
+                self._xbufs.clear()
+            specs = [((B, lim), torch.int32), ((B,), torch.int32)]
+            arena, (out, cnt), offs = _arena(self.device, specs, first=2)
+            host = torch.empty(arena.numel(), dtype=torch.uint8, pin_memory=True)
+            x_host = torch.empty((B, n_in), dtype=torch.int32, pin_memory=True)
+            x_dev = torch.empty((B, n_in), dtype=torch.int32, device=self.device)
+            b = (specs, offs, arena, out, cnt, host, host.numpy(), x_host, x_host.numpy(), x_dev)
+            self._xbufs[key] = b
+        specs, offs, arena, out, cnt, host, host_np, x_host, x_host_np, x_dev = b
+        np.copyto(x_host_np, idx, casting="same_kind")
+        with torch.cuda.device(self.device), devtime.span(None, self.device):
+            x_dev.copy_(x_host, non_blocking=True)
+            nat.check(nat.lib().ahr_graph_expand(self._h, ACTIONS[action], nat.ptr(x_dev), B, n_in, int(limit),
+                                                 nat.ptr(out), nat.ptr(cnt), nat.stream_ptr(None)),
+                      "ahr_graph_expand")
+            host.copy_(arena, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+        o, c = _host_views(host_np, specs, offs)
+        return o.copy(), c.copy()
+
 
 @dataclass
 class RerankParams:
@@ -422,6 +454,29 @@ class SearchEngine:
         rows = np.asarray([graph.index.get(r, n + i) for i, r in enumerate(self.row_ids)], np.int32)
         self.row_to_node_host = rows if len(rows) else np.zeros(1, np.int32)
         self.row_to_node = torch.from_numpy(self.row_to_node_host).to(graph.device)
+        self._bufs: Dict[Tuple, Tuple] = {}
+
+    _BUF_SHAPES = 8  # result-buffer sets kept (one per batch shape / search parameter shape)
+
+    def _buffers(self, specs, B: int, dim: int):
+        """The device buffer of a search's outputs (dense scores / rows + the eight rerank arrays),
+        its pinned host copy and a pinned + device query staging pair, per shape, reused across
+        calls: run() synchronises before it returns, so no call touches a buffer a previous one
+        still uses (one caller at a time per engine, like the reference's search())."""
+        key = (tuple(specs), dim)
+        b = self._bufs.get(key)
+        if b is None:
+            if len(self._bufs) >= self._BUF_SHAPES:
+                self._bufs.clear()
+            dev = self.graph.device
+            arena, (scores, rows), offs = _arena(dev, specs, first=2)
+            host = torch.empty(arena.numel(), dtype=torch.uint8, pin_memory=True)
+            q_host = torch.empty((B, dim), dtype=torch.float32, pin_memory=True)
+            q_dev = torch.empty((B, dim), dtype=torch.float32, device=dev)
+            b = (arena, scores, rows, offs, [arena.data_ptr() + o for o in offs[2:]], host, host.numpy(),
+                 q_host, q_host.numpy(), q_dev)
+            self._bufs[key] = b
+        return b
 
     def node_id(self, idx: int) -> str:
         n = self.graph.n_nodes
@@ -439,16 +494,22 @@ class SearchEngine:
         dev = self.graph.device
         specs = [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)] + self.graph.rerank_specs(
             B, k_dense, params)
-        arena, (scores, rows), offs = _arena(dev, specs, first=2)
-        base = arena.data_ptr()
+        dim = int(query_vectors.shape[-1])
+        arena, scores, rows, offs, out_ptrs, host_t, host_np, q_host, q_host_np, q_dev = self._buffers(specs, B, dim)
+        if query_vectors.device.type == "cpu":  # staged in pinned memory, copied on the current stream
+            np.copyto(q_host_np, query_vectors.reshape(B, dim).numpy(), casting="same_kind")
+            q_dev.copy_(q_host, non_blocking=True)
+            query_vectors = q_dev
         with devtime.span(None, dev):  # (recorded on the current stream, after the waits)
             self.index.query(query_vectors, k_dense, stream=stream, out=(scores, rows))
             max_exp = specs[2][0][1]  # rerank_specs: exp_nodes is [B, max_exp]
-            self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, max_exp,
-                                          [base + o for o in offs[2:]], arena, stream=stream)
+            self.graph.expand_rerank_rows(rows, scores, self.row_to_node, params, max_exp, out_ptrs, arena,
+                                          stream=stream)
             if stream is not None:  # the host copy runs on the current stream
                 torch.cuda.current_stream(dev).wait_stream(stream)
-        (host_buf,) = to_host_arrays(arena)
-        scores_h, rows_h, *outs = _host_views(host_buf, specs, offs)
+        host_t.copy_(arena, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        # (copies: the host buffer is the next call's)
+        scores_h, rows_h, *outs = [v.copy() for v in _host_views(host_np, specs, offs)]
         host = RerankResult(*outs)
         return rows_h, scores_h, host
