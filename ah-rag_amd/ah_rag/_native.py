@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = (
     "ahr_index_set_debug_flags", "ahr_index_set_workspace",
     "ahr_index_query", "ahr_index_query_keys", "ahr_index_scores", "ahr_topk_merge", "ahr_key_decode",
     "ahr_graph_create", "ahr_graph_destroy", "ahr_graph_expand_rerank", "ahr_graph_expand_rerank_rows",
-    "ahr_graph_expand",
+    "ahr_graph_expand", "ahr_graph_expand_ws_bytes", "ahr_graph_expand_host",
     "ahr_graph_lca", "ahr_graph_lca_workspace", "ahr_graph_lca_large", "ahr_graph_info",
 )
 
@@ -116,6 +116,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_graph_expand_rerank_rows": ([_P, _P, _P, _L, _P, _I, _I, ctypes.POINTER(RerankParams), _I,
                                           _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
         "ahr_graph_expand": ([_P, _I, _P, _I, _I, _I, _P, _P, _P], _I),
+        "ahr_graph_expand_ws_bytes": ([_I, _I, _I, _P], _I),
+        "ahr_graph_expand_host": ([_P, _I, _P, _I, _I, _I, _P, _P, _P, _L, _P], _I),
         "ahr_graph_lca": ([_P, _P, _I, _I, _I, _P, _P, _P], _I),
         "ahr_graph_lca_workspace": ([_P, _I, _P], _I),
         "ahr_graph_lca_large": ([_P, _P, _I, _I, _I, _P, _P, _P, _L, _P], _I),

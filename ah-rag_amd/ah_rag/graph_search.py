@@ -264,9 +264,10 @@ class DeviceGraph:
 
     def expand_host(self, action: str, idx: np.ndarray, limit: int = 10) -> Tuple[np.ndarray, np.ndarray]:
         """expand() of host node indices (int32 [B, n_in], -1 = skip) with host results (out
-        [B, max(limit, 1)], count [B]): the inputs staged in pinned memory and both outputs read
-        back in one copy, with buffers kept per shape and reused (one caller at a time: the
-        single-environment step), one stream sync."""
+        [B, max(limit, 1)], count [B]) through ahr_graph_expand_host: one C call copies the inputs
+        in, expands, copies both outputs back and waits. Pinned host buffers and the device
+        workspace are kept per shape and reused (one caller at a time: the single-environment
+        step)."""
         B, n_in = idx.shape
         lim = max(limit, 1)
         key = (B, n_in, lim)
@@ -274,25 +275,23 @@ class DeviceGraph:
         if b is None:
             if len(self._xbufs) >= 8:
                 self._xbufs.clear()
-            specs = [((B, lim), torch.int32), ((B,), torch.int32)]
-            arena, (out, cnt), offs = _arena(self.device, specs, first=2)
-            host = torch.empty(arena.numel(), dtype=torch.uint8, pin_memory=True)
+            need = nat.ctypes.c_int64()
+            nat.check(nat.lib().ahr_graph_expand_ws_bytes(B, n_in, int(limit), nat.ctypes.byref(need)),
+                      "ahr_graph_expand_ws_bytes")
+            ws_bytes = need.value
+            ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=self.device)
             x_host = torch.empty((B, n_in), dtype=torch.int32, pin_memory=True)
-            x_dev = torch.empty((B, n_in), dtype=torch.int32, device=self.device)
-            b = (specs, offs, arena, out, cnt, host, host.numpy(), x_host, x_host.numpy(), x_dev)
+            res = torch.empty(B * lim + B, dtype=torch.int32, pin_memory=True)  # out [B][lim], then count [B]
+            b = (ws, ws_bytes, x_host, x_host.numpy(), res, res.numpy())
             self._xbufs[key] = b
-        specs, offs, arena, out, cnt, host, host_np, x_host, x_host_np, x_dev = b
-        np.copyto(x_host_np, idx, casting="same_kind")
-        with torch.cuda.device(self.device), devtime.span(None, self.device):
-            x_dev.copy_(x_host, non_blocking=True)
-            nat.check(nat.lib().ahr_graph_expand(self._h, ACTIONS[action], nat.ptr(x_dev), B, n_in, int(limit),
-                                                 nat.ptr(out), nat.ptr(cnt), nat.stream_ptr(None)),
-                      "ahr_graph_expand")
-            host.copy_(arena, non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
-        o, c = _host_views(host_np, specs, offs)
-        return o.copy(), c.copy()
-
+        ws, ws_bytes, x_host, x_np, res, res_np = b
+        np.copyto(x_np, idx, casting="same_kind")
+        with devtime.span(None, self.device):
+            nat.check(nat.lib().ahr_graph_expand_host(
+                self._h, ACTIONS[action], nat.ptr(x_host), B, n_in, int(limit), nat.ptr(res),
+                nat.ptr(res) + 4 * B * lim, nat.ptr(ws), ws_bytes,
+                nat.stream_ptr(torch.cuda.current_stream(self.device))), "ahr_graph_expand_host")
+        return res_np[:B * lim].reshape(B, lim).copy(), res_np[B * lim:].copy()
 
 @dataclass
 class RerankParams:

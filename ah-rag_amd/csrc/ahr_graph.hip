@@ -644,4 +644,47 @@ int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int
   return AHR_OK;
 }
 
+// workspace layout: inputs [B][n_in], out [B][max(limit, 1)], count [B] (int32, 256-B aligned parts)
+static int64_t expand_ws_bytes(int B, int n_in, int limit) {
+  auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+  return al((int64_t)B * n_in * 4) + al((int64_t)B * (limit > 0 ? limit : 1) * 4) + al((int64_t)B * 4);
+}
+
+int ahr_graph_expand_ws_bytes(int B, int n_in, int limit, int64_t* bytes) {
+  if (!bytes) return fail(AHR_EINVAL, "null output");
+  if (B < 0 || n_in < 0 || limit < 0) return fail(AHR_EINVAL, "negative size");
+  *bytes = expand_ws_bytes(B, n_in, limit);
+  return AHR_OK;
+}
+
+int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, int B, int n_in, int limit,
+                          int32_t* host_out, int32_t* host_count, void* ws, int64_t ws_bytes, void* stream) {
+  if (!g) return fail(AHR_EINVAL, "null graph");
+  if (action < 0 || action > 2) return fail(AHR_EINVAL, "action must be 0, 1 or 2");
+  if (B < 0 || n_in < 0 || limit < 0) return fail(AHR_EINVAL, "negative size");
+  if (B == 0) return AHR_OK;
+  if ((n_in > 0 && !host_inputs) || !host_count || !host_out || !ws) return fail(AHR_EINVAL, "null buffer");
+  if (ws_bytes < expand_ws_bytes(B, n_in, limit)) return fail(AHR_EINVAL, "workspace too small");
+  DeviceGuardG dg(g->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int lim = limit > 0 ? limit : 1;
+  auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+  int32_t* d_in = static_cast<int32_t*>(ws);
+  int32_t* d_out = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + al((int64_t)B * n_in * 4));
+  int32_t* d_cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d_out) + al((int64_t)B * lim * 4));
+  if (n_in > 0) AHR_HIP(hipMemcpyAsync(d_in, host_inputs, (size_t)B * n_in * 4, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(expand_kernel, dim3((B + 63) / 64), dim3(64), 0, s, g->dg, action, d_in, B, n_in, limit,
+                     d_out, d_cnt);
+  AHR_HIP(hipGetLastError());
+  // out and count are adjacent (count after out's padded part): one copy when out needs no padding
+  if ((int64_t)B * lim * 4 == al((int64_t)B * lim * 4) && host_count == host_out + (int64_t)B * lim) {
+    AHR_HIP(hipMemcpyAsync(host_out, d_out, (size_t)B * lim * 4 + (size_t)B * 4, hipMemcpyDeviceToHost, s));
+  } else {
+    AHR_HIP(hipMemcpyAsync(host_out, d_out, (size_t)B * lim * 4, hipMemcpyDeviceToHost, s));
+    AHR_HIP(hipMemcpyAsync(host_count, d_cnt, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+  }
+  AHR_HIP(hipStreamSynchronize(s));
+  return AHR_OK;
+}
+
 }  // extern "C"

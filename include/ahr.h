@@ -274,6 +274,17 @@ int ahr_graph_expand_rerank_rows(ahr_graph* g, const int32_t* rows, const int32_
 int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int n_in,
                      int limit, int32_t* out, int32_t* out_count, void* stream);
 
+/* ahr_graph_expand from host memory to host memory in one call (the single environment's step,
+ * environment.py:393-480 one query at a time): copies host_inputs [B][n_in] into the device
+ * workspace, expands, copies out [B][max(limit, 1)] and out_count [B] back into host_out /
+ * host_count and waits for the stream. ws: device memory of at least the *bytes that
+ * ahr_graph_expand_ws_bytes(B, n_in, limit, &bytes) returns (host-only arithmetic). Host buffers should be pinned (hipHostMalloc / torch pin_memory) for
+ * asynchronous copies; pageable ones work, slower. */
+int ahr_graph_expand_ws_bytes(int B, int n_in, int limit, int64_t* bytes);
+int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, int B, int n_in,
+                          int limit, int32_t* host_out, int32_t* host_count, void* ws, int64_t ws_bytes,
+                          void* stream);
+
 /* Batched GraphEnvironment.expand_to_lca (environment.py:243-299): per query the nodes of the
  * intersection of the inputs' "ancestors or self" sets on the belongs_to DAG (nx.ancestors: nodes
  * with a belongs_to path to the input) that have no belongs_to out-edge to another member.

@@ -79,6 +79,22 @@ def test_graph_create_validates_csr_before_the_device():
     assert lib.ahr_graph_expand(None, 0, None, 1, 1, 10, None, None, None) == nat.AHR_EINVAL
 
 
+def test_expand_host_validation_and_workspace_size():
+    """ahr_graph_expand_host's argument checks and ahr_graph_expand_ws_bytes' layout (inputs,
+    out [B][max(limit, 1)], count [B], each part rounded up to 256 B): host arithmetic only."""
+    nat, lib = _lib()
+    n = ctypes.c_int64()
+    assert lib.ahr_graph_expand_ws_bytes(1, 3, 10, ctypes.byref(n)) == nat.AHR_OK
+    assert n.value == 256 * 3
+    assert lib.ahr_graph_expand_ws_bytes(100, 3, 0, ctypes.byref(n)) == nat.AHR_OK
+    assert n.value == 1280 + 512 + 512  # 1200 B inputs, out of width 1, 400 B counts
+    assert lib.ahr_graph_expand_ws_bytes(-1, 3, 10, ctypes.byref(n)) == nat.AHR_EINVAL
+    assert lib.ahr_graph_expand_ws_bytes(1, 3, 10, None) == nat.AHR_EINVAL
+    buf = (ctypes.c_int32 * 64)()
+    assert lib.ahr_graph_expand_host(None, 0, buf, 1, 3, 10, buf, buf, buf, 4096, None) == nat.AHR_EINVAL
+    assert b"graph" in lib.ahr_last_error()
+
+
 def test_key_decode_edge_values():
     nat, lib = _lib()
     from ah_rag.distributed import encode_keys_host
