@@ -1,7 +1,8 @@
 """Device expand_to_lca (ahr_graph_lca) against the oracle's restatement of the reference
 (oracle/search_ref.env_lca <- environment.py:243-299) on the reference's own saved graph, batched
 over many input lists: single inputs, duplicates, summaries of both levels, entity/summary mixes,
-padding; plus queries beyond the LDS kernel's tables, answered by the global-memory kernel."""
+padding; plus queries beyond the LDS kernel's tables, answered by the global-memory kernel; and
+the host-to-host expansion entry (ahr_graph_expand_host) against the device one."""
 import os
 
 import numpy as np
@@ -85,3 +86,29 @@ def test_lca_over_capacity_matches_oracle(cuda):
     want, _ = search_ref.env_lca(G, [top, mids[0]])
     assert [x["node_id"] for x in obs["selection"]] == want and info["lca_count"] == len(want)
     assert isinstance(hg.G, nx.DiGraph)
+
+
+def test_expand_host_matches_device_expand(cuda):
+    """ahr_graph_expand_host (host in, host out, one call; reused per-shape buffers) returns what
+    ahr_graph_expand writes on the device, for every action, ragged inputs (-1 padding), limits 0,
+    1 and 10, and batch shapes met more than once (the buffers are reused)."""
+    import torch
+    from ah_rag.graph.hierarchical_graph import HierarchicalGraph
+    hg = HierarchicalGraph.load(os.path.join(GOLDEN, "reference_graph"))
+    dg = hg.device_graph()
+    nodes = list(hg.G.nodes)
+    rng = np.random.default_rng(11)
+    for rep in range(2):
+        for action in ("parents", "children", "related"):
+            for B, n_in, limit in ((1, 3, 10), (1, 1, 1), (7, 5, 10), (64, 2, 0), (33, 4, 3)):
+                idx = np.full((B, n_in), -1, np.int32)
+                for b in range(B):
+                    m = int(rng.integers(0, n_in + 1))
+                    idx[b, :m] = dg.node_indices([nodes[int(i)] for i in rng.integers(0, len(nodes), m)])
+                out_h, cnt_h = dg.expand_host(action, idx, limit)
+                out_d, cnt_d = dg.expand(action, torch.from_numpy(idx), limit)
+                cnt_d = cnt_d.cpu().numpy()
+                out_d = out_d.cpu().numpy()
+                assert np.array_equal(cnt_h, cnt_d), (action, B, n_in, limit)
+                for b in range(B):
+                    assert np.array_equal(out_h[b, :cnt_h[b]], out_d[b, :cnt_d[b]]), (action, B, b)
