@@ -3,7 +3,7 @@
 Same constructor, actions, observation and info dicts. The differences are where the time goes:
   * neighbour expansions (expand_parents / expand_children / expand_related, reference :393-480)
     run as the batched HIP kernel ahr_graph_expand over the device CSR (B = 1 here;
-    VecGraphEnvironment in ah_rag.agent.vec_env batches them across environments);
+    VecAHRAGGymEnv in ah_rag.agent.vec_env batches them across environments);
   * semantic_anchor goes through HierarchicalGraph.search (dense top-k + expansion + rerank on the
     GPU);
   * the node/edge counts every observation reports (reference :136-139, an O(N) networkx walk per
@@ -41,7 +41,7 @@ class GraphEnvironment:
                  debug: bool = False, log_level: str = "normal", redact: bool = True, *,
                  graph: Optional[HierarchicalGraph] = None) -> None:
         """`graph` (keyword-only, not in the reference) shares an already loaded graph, e.g. across
-        the environments of a VecGraphEnvironment, instead of loading graph_dir again."""
+        the environments of a VecAHRAGGymEnv, instead of loading graph_dir again."""
         self.graph_dir = graph_dir
         self.random_state = random_state
         self.hg: Optional[HierarchicalGraph] = graph
@@ -77,7 +77,9 @@ class GraphEnvironment:
     # ---- plumbing ----------------------------------------------------------------------------
     def _ensure_graph_loaded(self) -> None:
         if self.hg is None:
-            self.hg = HierarchicalGraph.load(self.graph_dir)
+            # environments of one graph directory share the loaded graph and its device structures
+            # (read-only here; HierarchicalGraph.load_shared, AHR_SHARE_GRAPH=0: a private load each)
+            self.hg = HierarchicalGraph.load_shared(self.graph_dir)
 
     def _log(self, event: Dict[str, Any]) -> None:
         if self.logging_enabled and self.logger is not None:

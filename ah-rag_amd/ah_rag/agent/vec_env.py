@@ -86,6 +86,7 @@ class _ObsBatch:
         self.alias: Optional[List[Optional[Tuple["_ObsBatch", int]]]] = None
         self.cache: Dict[int, Dict[str, Any]] = {}
         self.search = None  # reset: (engine, params, rows, scores, res, seed_idx, seed_sem, seed_n)
+        self.stamp = None   # the graph version the observation was taken on (HierarchicalGraph._graph_stamp)
 
     def copy_rows(self, src: "_ObsBatch", idx: Optional[np.ndarray] = None) -> None:
         """src's rows idx into this batch (idx None: every row)."""
@@ -139,6 +140,18 @@ class _GraphEnvView:
     @property
     def step_count(self) -> int:
         return int(self._v._steps[self._e])
+
+    def end_episode(self, *_, **__):
+        raise NotImplementedError("VecAHRAGGymEnv keeps no per-environment GraphEnvironment: step the environment "
+                                  "with action 5 (end_episode) instead")
+
+    @property
+    def stats(self):
+        raise NotImplementedError("VecAHRAGGymEnv does not keep GraphEnvironment's per-action stats log")
+
+    @property
+    def session_path(self):
+        raise NotImplementedError("VecAHRAGGymEnv writes no per-environment session log")
 
     @property
     def selection_set(self) -> set:
@@ -243,6 +256,13 @@ class VecAHRAGGymEnv:
         return out
 
     # ---- lazily built dicts --------------------------------------------------------------------
+    def _check_stamp(self, ob: _ObsBatch) -> None:
+        """A dict is built on first access from the live graph's attributes; if the graph changed
+        since the step that produced the observation, it would mix two graph versions, so refuse."""
+        if ob.stamp is not None and ob.stamp != self.hg._graph_stamp():
+            raise RuntimeError("the graph changed after this observation was taken: its info dicts can no longer be "
+                               "built as the step would have returned them (read info[i] before mutating the graph)")
+
     def _briefs(self, idx: np.ndarray, n: int, score, sem) -> List[Dict[str, Any]]:
         ids = [self._id(i) for i in idx[:n].tolist()]
         sc = [score] * n if not isinstance(score, np.ndarray) else score[:n].tolist()
@@ -256,6 +276,7 @@ class VecAHRAGGymEnv:
         d = ob.cache.get(e)
         if d is not None:
             return d
+        self._check_stamp(ob)
         g = self._genv
         kind, n, step = int(ob.kind[e]), int(ob.sel_n[e]), int(ob.step[e])
         if kind == OBS_DETAILS:
@@ -285,6 +306,7 @@ class VecAHRAGGymEnv:
         key = ("cluster", e)
         c = ob.cache.get(key)
         if c is None:
+            self._check_stamp(ob)
             engine, params, rows, scores, res = ob.search[:5]
             c = ob.cache[key] = self.hg._assemble(engine, rows[e], scores[e], res, e, params.top_k, True)
         return c
@@ -324,6 +346,7 @@ class VecAHRAGGymEnv:
         seed_sem = 1.0 - (np.float32(1.0) - np.asarray(scores, np.float32)).astype(np.float64)
         ob.seed_n[:] = seed_n
         ob.search = (engine, params, rows, scores, res, seed_idx, seed_sem, seed_n)
+        ob.stamp = self.hg._graph_stamp()
         # selection cleared; frontier = the reranked nodes
         self._S = [_EMPTY] * E
         self._F = [frozenset(r[:c]) for r, c in zip(ob.sel.tolist(), n_out.tolist())]
@@ -356,6 +379,7 @@ class VecAHRAGGymEnv:
         ob.copy_rows(prev)  # the defaults: unchanged (aliased) observations
         ob.alias = [None] * E
         ob.search = prev.search
+        ob.stamp = self.hg._graph_stamp()
         pos = np.arange(K_NODES)[None, :]
         top_valid = pos < prev.sel_n[:, None]
 

@@ -27,6 +27,7 @@ import hashlib
 import itertools
 import json
 import os
+import weakref
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import networkx as nx
@@ -49,6 +50,24 @@ ROWS_FILE = "ahr_rows.json"
 # Process-wide version numbers of resident indexes: a cache keyed on one can never match a later
 # index (an id() can be reused once the old object is gone, and a per-object counter restarts).
 _INDEX_VERSIONS = itertools.count(1)
+
+# Process-wide sharing of what is derived from files (the reference's PPO loop builds every
+# environment with AHRAGGymEnv(graph_dir=...), each loading the graph and opening the store again,
+# scripts/train_ppo.py:25-26): the HBM copy of a vector store per (store path, storage type, GPU),
+# the device graph per (saved graph file, GPU) while a loaded graph is unmodified, and the loaded
+# graph itself per graph directory for the environments (HierarchicalGraph.load_shared). Weak
+# values: an entry lives as long as some graph object uses it.
+_RESIDENT: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+_DEVICE_GRAPHS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+_SHARED_GRAPHS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+
+
+def _file_stamp(path: str) -> Tuple:
+    try:
+        st = os.stat(path)
+        return (st.st_mtime_ns, st.st_size)
+    except OSError:
+        return (0, 0)
 
 
 def _sha(text: str) -> str:
@@ -198,6 +217,7 @@ class HierarchicalGraph:
         self.G.graph.setdefault("vector_index", {"db_path": "vector_db", "model": DEFAULT_MODEL,
                                                  "indexed_nodes": 0, "indexed_meta": {}})
         self._version = 0
+        self._source: Optional[Tuple] = None  # (saved structure file, its stamp, node count) after load()
         self._dev_graph: Optional[Tuple[Tuple, DeviceGraph]] = None
         self._indexes: Dict[str, ResidentIndex] = {}
         self._engines: Dict[str, Tuple[Tuple, SearchEngine]] = {}
@@ -423,7 +443,26 @@ class HierarchicalGraph:
             json.dump(out, f, ensure_ascii=False, indent=2)
 
     @classmethod
+    def load_shared(cls, directory: str = GRAPH_DIR) -> "HierarchicalGraph":
+        """load(directory), shared by every caller in the process while the saved files and the
+        loaded graph are unchanged: GraphEnvironment / AHRAGGymEnv(graph_dir=...) use it, so the
+        environments of one training loop parse the graph (seconds at 130k nodes) and build its
+        device structures once. The environment API only reads the graph; a graph changed through
+        add_* is not handed out again. AHR_SHARE_GRAPH=0 gives every caller its own load()."""
+        if os.environ.get("AHR_SHARE_GRAPH", "1") == "0":
+            return cls.load(directory)
+        d = os.path.abspath(directory)
+        key = (d, _file_stamp(os.path.join(d, "structure.json")), _file_stamp(os.path.join(d, "meta.json")))
+        hg = _SHARED_GRAPHS.get(key)
+        if hg is None or hg._version != 0 or hg._source is None or len(hg.G) != hg._source[2]:
+            hg = cls.load(directory)
+            _SHARED_GRAPHS[key] = hg
+        return hg
+
+    @classmethod
     def load(cls, directory: str = GRAPH_DIR) -> "HierarchicalGraph":
+        spath = os.path.abspath(os.path.join(directory, "structure.json"))
+        stamp = _file_stamp(spath)
         with open(os.path.join(directory, "structure.json"), encoding="utf-8") as f:
             data = json.load(f)
         hg = cls()
@@ -451,6 +490,7 @@ class HierarchicalGraph:
                     hg.G.graph["dirty"] = meta["dirty"]
             except Exception:
                 pass
+        hg._source = (spath, stamp, len(hg.G))
         return hg
 
     def _graph_snapshot_hash(self) -> str:
@@ -600,13 +640,12 @@ class HierarchicalGraph:
                                                              normalize_embeddings=True), np.float32)
         store.upsert(todo, vectors, metas)
         store.save(model_name)
-        # the resident HBM copy follows the same upsert (changed rows only); a reset drops it
-        resident = self._indexes.get(os.path.abspath(db_path))
+        # the resident HBM copy (shared by every graph object on this store) follows the same upsert
+        # (changed rows only); after a reset it is reloaded from the rewritten store
+        resident = self._indexes.get(os.path.abspath(db_path)) or _RESIDENT.get(self._resident_key(db_path))
         if resident is not None:
             if reset:
-                resident.close()
-                self._indexes.pop(os.path.abspath(db_path))
-                self._engines.pop(os.path.abspath(db_path), None)
+                resident.reload()
             else:
                 resident.apply(todo, vectors, metas)
         new_meta = dict(prev)
@@ -623,18 +662,37 @@ class HierarchicalGraph:
     def device_graph(self) -> DeviceGraph:
         stamp = self._graph_stamp()
         if self._dev_graph is None or self._dev_graph[0] != stamp:
-            self._dev_graph = (stamp, DeviceGraph(self.G))
+            dev = torch.device("cuda", torch.cuda.current_device())
+            # a graph unchanged since load() shares the device graph of every other load of the same
+            # saved file (same content, same networkx order)
+            shared = self._source is not None and self._version == 0 and len(self.G) == self._source[2]
+            key = (self._source[:2], dev.index) if shared else None
+            dg = _DEVICE_GRAPHS.get(key) if shared else None
+            if dg is None:
+                dg = DeviceGraph(self.G, dev)
+                if shared:
+                    _DEVICE_GRAPHS[key] = dg
+            self._dev_graph = (stamp, dg)
             self._engines.clear()
         return self._dev_graph[1]
 
+    def _resident_key(self, db_path: str) -> Tuple:
+        return (os.path.abspath(db_path), os.environ.get("AHR_INDEX_DTYPE", "f32"), torch.cuda.current_device())
+
     def resident_index(self, db_path: str) -> ResidentIndex:
-        """The store at db_path resident in HBM; reloaded whole only when another writer changed
-        the file (build_vector_index keeps it current incrementally)."""
+        """The store at db_path resident in HBM (one copy per store, storage type and GPU in the
+        process, shared by every graph object); reloaded whole only when another writer changed the
+        file (build_vector_index keeps it current incrementally)."""
         key = os.path.abspath(db_path)
         res = self._indexes.get(key)
         if res is None:
-            res = self._indexes[key] = ResidentIndex(key, self.device_graph().device)
-        elif res.stamp != store_stamp(key):
+            rkey = self._resident_key(key)
+            res = _RESIDENT.get(rkey)
+            if res is None:
+                res = ResidentIndex(key, self.device_graph().device)
+                _RESIDENT[rkey] = res
+            self._indexes[key] = res
+        if res.stamp != store_stamp(key):
             res.reload()
         return res
 

@@ -22,6 +22,7 @@ import functools
 import itertools
 import json
 import math
+import threading
 from dataclasses import dataclass
 from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -88,6 +89,7 @@ class DeviceGraph:
     def __init__(self, G: nx.DiGraph, device: Optional[torch.device] = None) -> None:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self._xbufs: Dict[Tuple[int, int, int], Tuple] = {}  # expand_host's buffers per shape
+        self._xlock = threading.Lock()  # expand_host: one caller at a time on the reused buffers
         self.serial = next(_GRAPH_SERIALS)
         self.ids: List[str] = list(G.nodes)
         self.index: Dict[str, int] = {nid: i for i, nid in enumerate(self.ids)}
@@ -266,8 +268,12 @@ class DeviceGraph:
         """expand() of host node indices (int32 [B, n_in], -1 = skip) with host results (out
         [B, max(limit, 1)], count [B]) through ahr_graph_expand_host: one C call copies the inputs
         in, expands, copies both outputs back and waits. Pinned host buffers and the device
-        workspace are kept per shape and reused (one caller at a time: the single-environment
-        step)."""
+        workspace are kept per shape and reused; a lock makes concurrent callers (threads sharing
+        one graph) take turns, so none overwrites another's staged inputs or results."""
+        with self._xlock:
+            return self._expand_host(action, idx, limit)
+
+    def _expand_host(self, action: str, idx: np.ndarray, limit: int) -> Tuple[np.ndarray, np.ndarray]:
         B, n_in = idx.shape
         lim = max(limit, 1)
         key = (B, n_in, lim)
@@ -306,6 +312,24 @@ class RerankParams:
     member_top_m: int
     top_k: int
 
+    def key(self) -> Tuple:
+        boost = self.layer_boost or {}
+        tf = None if not self.type_filter else tuple(self.type_filter)
+        return (self.alpha, self.beta, self.gamma, self.delta, self.judge_min, self.confidence_min,
+                tuple(sorted(((str(k), k is None), float(v)) for k, v in boost.items())), tf,
+                int(self.member_top_m), int(max(self.top_k, 0)))
+
+    def to_c_cached(self) -> nat.RerankParams:
+        """to_c() of these values, built once per distinct parameter set (the drop-in search resolves
+        the same defaults on every call). The struct is shared: callers must not modify it."""
+        k = self.key()
+        c = _C_PARAMS.get(k)
+        if c is None:
+            if len(_C_PARAMS) >= 256:
+                _C_PARAMS.clear()
+            c = _C_PARAMS[k] = self.to_c()
+        return c
+
     def to_c(self) -> nat.RerankParams:
         c = nat.RerankParams()
         c.alpha, c.beta, c.gamma, c.delta = (float(self.alpha), float(self.beta), float(self.gamma),
@@ -324,6 +348,9 @@ class RerankParams:
         c.member_top_m = int(self.member_top_m)
         c.top_k = int(max(self.top_k, 0))
         return c
+
+
+_C_PARAMS: Dict[Tuple, nat.RerankParams] = {}
 
 
 @dataclass
@@ -440,6 +467,18 @@ def resolve_search_params(stored: Dict[str, Any], top_k: int, member_top_m: Opti
         top_k=top_k)
 
 
+def _index_lock(index) -> threading.Lock:
+    """One lock per DenseIndex (its query workspaces and the engines' reused buffers)."""
+    lk = getattr(index, "_ahr_engine_lock", None)
+    if lk is None:
+        lk = threading.RLock()
+        try:
+            index._ahr_engine_lock = lk
+        except AttributeError:
+            pass
+    return lk
+
+
 class SearchEngine:
     """DenseIndex (node vectors) + row->node map + DeviceGraph: the batched search pipeline."""
 
@@ -454,6 +493,10 @@ class SearchEngine:
         self.row_to_node_host = rows if len(rows) else np.zeros(1, np.int32)
         self.row_to_node = torch.from_numpy(self.row_to_node_host).to(graph.device)
         self._bufs: Dict[Tuple, Tuple] = {}
+        self._hbufs: Dict[Tuple, Tuple] = {}
+        # the staging / result buffers are reused across calls: one caller at a time per index
+        # (engines over the same index share its workspaces too), concurrent callers take turns
+        self._lock = _index_lock(index)
 
     _BUF_SHAPES = 8  # result-buffer sets kept (one per batch shape / search parameter shape)
 
@@ -481,9 +524,56 @@ class SearchEngine:
         n = self.graph.n_nodes
         return self.graph.ids[idx] if idx < n else self.row_ids[idx - n]
 
+    HOST_PATH_MAX_B = 64  # host query batches up to this size take ahr_search_host (one C call)
+
     def run(self, query_vectors: torch.Tensor, params: RerankParams,
             stream: Optional[torch.cuda.Stream] = None) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
         """Dense top_k -> expansion -> rerank for a batch. Returns host (rows, scores, result)."""
+        with self._lock:
+            if stream is None and query_vectors.device.type == "cpu" and \
+                    1 <= (query_vectors.shape[0] if query_vectors.dim() > 1 else 1) <= self.HOST_PATH_MAX_B:
+                return self._run_host(query_vectors, params)
+            return self._run(query_vectors, params, stream)
+
+    def _run_host(self, query_vectors: torch.Tensor, params: RerankParams
+                  ) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
+        """A small host batch through ahr_search_host: query copy, dense top-k, expansion + rerank,
+        result copy and stream wait in one C call, on the current stream (the drop-in search())."""
+        B = int(query_vectors.shape[0]) if query_vectors.dim() > 1 else 1
+        dim = int(query_vectors.shape[-1])
+        k_dense = min(max(1, params.top_k), max(1, len(self.index)), nat.AHR_MAX_K_LARGE)
+        max_exp = max(1, k_dense * (1 + max(2, params.member_top_m)))
+        kk = max(max(params.top_k, 0), 1)
+        key = (B, dim, k_dense, max_exp, kk)
+        b = self._hbufs.get(key)
+        if b is None:
+            if len(self._hbufs) >= self._BUF_SHAPES:
+                self._hbufs.clear()
+            offs = (nat.ctypes.c_int64 * 10)()
+            ws_b, ar_b = nat.ctypes.c_int64(), nat.ctypes.c_int64()
+            nat.check(nat.lib().ahr_search_layout(B, dim, k_dense, max_exp, kk, offs, nat.ctypes.byref(ws_b),
+                                                  nat.ctypes.byref(ar_b)), "ahr_search_layout")
+            ws = torch.empty(ws_b.value, dtype=torch.uint8, device=self.graph.device)
+            q_host = torch.empty((B, dim), dtype=torch.float32, pin_memory=True)
+            out = torch.empty(ar_b.value, dtype=torch.uint8, pin_memory=True)
+            specs = [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)] + self.graph.rerank_specs(
+                B, k_dense, params)
+            views = _host_views(out.numpy(), specs, list(offs))
+            b = self._hbufs[key] = (ws, ws_b.value, q_host, q_host.numpy(), out, views)
+        ws, ws_bytes, q_host, q_np, out, views = b
+        np.copyto(q_np, query_vectors.reshape(B, dim).numpy(), casting="same_kind")
+        dev = self.graph.device
+        with devtime.span(None, dev):
+            nat.check(nat.lib().ahr_search_host(
+                self.index.handle, self.graph._h, q_host.data_ptr(), B, k_dense, self.row_to_node.data_ptr(),
+                int(self.row_to_node.shape[0]), nat.ctypes.byref(params.to_c_cached()), max_exp, ws.data_ptr(),
+                ws_bytes, out.data_ptr(), nat.stream_ptr(torch.cuda.current_stream(dev))), "ahr_search_host")
+        # (copies: the host buffer is the next call's)
+        scores_h, rows_h, *outs = [v.copy() for v in views]
+        return rows_h, scores_h, RerankResult(*outs)
+
+    def _run(self, query_vectors: torch.Tensor, params: RerankParams,
+             stream: Optional[torch.cuda.Stream] = None) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
         k = max(1, params.top_k)
         # rows past the index count come back as -1 anyway: ask for at most count (Chroma's
         # n_results clamp), so a small corpus answers any top_k

@@ -34,4 +34,56 @@ int ahr_device_count(int* n) {
   return AHR_OK;
 }
 
+// ---- the drop-in search() in one call (include/ahr.h ahr_search_host) ----------------------
+int ahr_search_layout(int B, int dim, int k_dense, int max_exp, int kk, int64_t offsets[10], int64_t* ws_bytes,
+                      int64_t* arena_bytes) {
+  if (!offsets || !ws_bytes || !arena_bytes) return ahr::fail(AHR_EINVAL, "null output");
+  if (B < 1 || dim < 1 || k_dense < 1 || max_exp < 1 || kk < 1) return ahr::fail(AHR_EINVAL, "sizes must be >= 1");
+  const int64_t b = B;
+  const int64_t part[10] = {b * k_dense * 4, b * k_dense * 4, b * max_exp * 4, b * max_exp * 8, b * max_exp * 4,
+                            b * 4,           b * kk * 4,      b * kk * 8,      b * kk * 8,      b * 4};
+  int64_t o = 0;
+  for (int i = 0; i < 10; ++i) {
+    offsets[i] = o;
+    o += (part[i] + 7) / 8 * 8;
+  }
+  *arena_bytes = o;
+  *ws_bytes = (b * dim * 4 + 255) / 256 * 256 + o;
+  return AHR_OK;
+}
+
+int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int k_dense,
+                    const int32_t* row_to_node, int64_t n_rows, const ahr_rerank_params* params, int max_exp,
+                    void* ws, int64_t ws_bytes, void* host_out, void* stream) {
+  if (!ix || !g || !params) return ahr::fail(AHR_EINVAL, "null index, graph or params");
+  if (!host_q || !row_to_node || !ws || !host_out) return ahr::fail(AHR_EINVAL, "null buffer");
+  int dim = 0, dt = 0, pd = 0;
+  int64_t cap = 0, rb = 0;
+  int st = ahr_index_info(ix, &dim, &dt, &cap, &pd, &rb);
+  if (st != AHR_OK) return st;
+  const int kk = params->top_k > 0 ? params->top_k : 1;
+  int64_t off[10], need = 0, arena = 0;
+  st = ahr_search_layout(B, dim, k_dense, max_exp, kk, off, &need, &arena);
+  if (st != AHR_OK) return st;
+  if (ws_bytes < need) return ahr::fail(AHR_EINVAL, "workspace smaller than ahr_search_layout's ws_bytes");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* q = static_cast<char*>(ws);
+  char* a = q + ((int64_t)B * dim * 4 + 255) / 256 * 256;
+  AHR_HIP(hipMemcpyAsync(q, host_q, (size_t)B * dim * 4, hipMemcpyHostToDevice, s));
+  float* scores = reinterpret_cast<float*>(a + off[0]);
+  int32_t* rows = reinterpret_cast<int32_t*>(a + off[1]);
+  st = ahr_index_query(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream);
+  if (st != AHR_OK) return st;
+  st = ahr_graph_expand_rerank_rows(g, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp,
+                                    reinterpret_cast<int32_t*>(a + off[2]), reinterpret_cast<double*>(a + off[3]),
+                                    reinterpret_cast<int32_t*>(a + off[4]), reinterpret_cast<int32_t*>(a + off[5]),
+                                    reinterpret_cast<int32_t*>(a + off[6]), reinterpret_cast<double*>(a + off[7]),
+                                    reinterpret_cast<double*>(a + off[8]), reinterpret_cast<int32_t*>(a + off[9]),
+                                    stream);
+  if (st != AHR_OK) return st;
+  AHR_HIP(hipMemcpyAsync(host_out, a, (size_t)arena, hipMemcpyDeviceToHost, s));
+  AHR_HIP(hipStreamSynchronize(s));
+  return AHR_OK;
+}
+
 }  // extern "C"

@@ -374,10 +374,14 @@ def cold_kernel_ms(ix, q, k: int, reps: int, dev, dirty: bool = False) -> float:
     return prof["ms_sum"]["tile_topk"] / max(1, prof["calls"])
 
 
-def read_traffic(kernel: str, workload: str, batch: int):
+def read_traffic(kernel: str, workload: str, batch: int, dt: int = None):
     """(per-launch HBM bytes of `kernel`, the summary file) from the newest committed PMC summary
-    (profiles/) measured on this workload and batch, else (None, None). A committed measurement,
-    not this run's: the file is reported beside the value."""
+    (profiles/) measured on this workload, batch and storage type (dt: 0 f32, 1 f16, 2 bf16; None =
+    the workload's default), else (None, None). A committed measurement, not this run's: the file is
+    reported beside the value. Summaries without a recorded "_dt" (before round 6) count as the
+    workload's default type, or fp32 for the fp32-only kernel."""
+    default_dt = 1 if workload == "synth5m" else 2
+    want = default_dt if dt is None else dt
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*", "pmc_traffic.json")), reverse=True)
     paths.append(os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     for path in paths:
@@ -387,6 +391,9 @@ def read_traffic(kernel: str, workload: str, batch: int):
         except Exception:
             continue
         if data.get("_workload", "hotpot90k") != workload or data.get("_batch", 1024) != batch:
+            continue
+        file_dt = data.get("_dt", 0 if kernel == "topk_small_f32_kernel" else default_dt)
+        if file_dt != want:
             continue
         v = data.get(kernel, {}).get("hbm_bytes_per_launch")
         if v is not None:
@@ -410,7 +417,7 @@ def roofline(plan: dict, dtype: str, B: int, n_rows: int, d: int, k: int, tile_m
     # small batches are bound by the corpus stream
     hbm_bound = flops / alg_bytes < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
     hbm_gbs = alg_bytes / (tile_ms * 1e-3) / 1e9
-    traffic, traffic_src = read_traffic(kname, workload, B)
+    traffic, traffic_src = read_traffic(kname, workload, B, {"f32": 0, "f16": 1, "bf16": 2}[dtype])
     return {
         "kernel": f"{kname} (fused {'VALU fma-chain' if kname == 'topk_small_f32_kernel' else 'MFMA'} "
                   f"Q.N^T + top-k, {plan['kernel']})",
@@ -459,6 +466,8 @@ def sub_line(args, dev, spec, dtype: str, workload: str, label: str) -> dict:
         exact, cpu = cpu_baseline_chunked(chunks(), q[:nq].cpu().numpy(), k, N, d)
     else:
         _, exact = numpy_topk_chunked(chunks(), q[:nq].cpu().numpy(), k)
+        if not args.no_cpu_baseline:  # the headline's host legs (B = 1024 and B = 1) on this corpus
+            cpu = cpu_baseline(rows.cpu().numpy(), q.cpu().numpy(), k, args.cpu_seconds / 2, workload)
     return {
         "workload": label,
         "value": round(B * steps / dt, 1), "unit": "queries/s", "steps": steps, "untimed_steps_before": warm,
@@ -730,15 +739,14 @@ def run(args) -> None:
             f_dt, f_prof, f_res = time_queries(f32, q, k, args.steps, args.warmup,
                                                args.inflight or auto_inflight(f32, B, k), dev)
             f_tile = f_prof["ms_sum"]["tile_topk"] / max(1, f_prof["calls"])
-            f_tf = 2.0 * B * N * d / (f_tile * 1e-3) / 1e12
+            f_plan = f32.plan(B, k)
             out["exact_fp32"] = {
                 "value": round(B * args.steps / f_dt, 1), "unit": "queries/s",
                 "ms_per_step": round(f_dt / args.steps * 1e3, 4),
                 "recall_at_10": round(recall_at_k(f_res[1][:nq].cpu().numpy().astype(np.int64), exact), 4),
-                "launch": f32.plan(B, k),
+                "launch": f_plan,
                 "tile_ms": round(f_tile, 4),
-                "roofline": {"bound": "mfma", "achieved": round(f_tf, 2), "peak": MFMA_PEAK_TFLOPS["f32"],
-                             "unit": "TFLOP/s", "frac": round(f_tf / MFMA_PEAK_TFLOPS["f32"], 4)},
+                "roofline": roofline(f_plan, "f32", B, N, d, k, f_tile, workload),
             }
             if not args.no_batch_sweep:
                 # B = 1 on the fp32 index: the drop-in search() / GraphEnvironment default

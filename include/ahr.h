@@ -266,6 +266,25 @@ int ahr_graph_expand_rerank_rows(ahr_graph* g, const int32_t* rows, const int32_
                                  int32_t* out_nodes, double* out_sem, double* out_score,
                                  int32_t* out_count, void* stream);
 
+/* The whole drop-in search() of a small host query batch in ONE call (hierarchical_graph.py:
+ * 709-789 after the encode: Chroma query :714, distance -> similarity :719-724, expansion and
+ * rerank :726-782): copy the fp32 queries in, ahr_index_query (top k_dense), expansion + rerank
+ * fed by its rows (ahr_graph_expand_rerank_rows), copy every result back into one host buffer,
+ * wait for the stream. One foreign-function call instead of one per stage.
+ * Layout (ahr_search_layout, host-only arithmetic): the device workspace ws holds the queries
+ * [B][dim] f32 at offset 0 (its part rounded up to 256 B), then the result arena; host_out
+ * receives the arena: scores f32 [B][k_dense], rows i32 [B][k_dense], exp_nodes i32 [B][max_exp],
+ * exp_sem f64 [B][max_exp], exp_src i32 [B][max_exp], exp_count i32 [B], out_nodes i32 [B][kk],
+ * out_sem f64 [B][kk], out_score f64 [B][kk], out_count i32 [B] (kk = max(params->top_k, 1)),
+ * each part starting at an 8-B aligned offset (offsets[0..9], relative to the arena).
+ * host_q / host_out should be pinned (asynchronous copies); pageable memory works, slower.
+ * max_exp must be >= k_dense * (1 + max(2, member_top_m)). */
+int ahr_search_layout(int B, int dim, int k_dense, int max_exp, int kk, int64_t offsets[10],
+                      int64_t* ws_bytes, int64_t* arena_bytes);
+int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int k_dense,
+                    const int32_t* row_to_node, int64_t n_rows, const ahr_rerank_params* params,
+                    int max_exp, void* ws, int64_t ws_bytes, void* host_out, void* stream);
+
 /* Batched environment expansions (environment.py:393-480).
  * action: 0 expand_parents, 1 expand_children, 2 expand_related.
  * inputs: device int32 [B][n_in] (-1 = absent / not in graph); out: device int32 [B][limit],

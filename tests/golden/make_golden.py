@@ -12,6 +12,9 @@ recording their outputs as data under tests/golden/:
   env_cases.json                              GraphEnvironment action scripts (R9-R11)
   gym_cases.json                              AHRAGGymEnv episodes (R10, R12)
   naive_cases.json                            NaiveRAG.run contexts (R13)
+  collection_cases.json                       every raw collection upsert / query the reference's
+                                              build_vector_index / search made for search_cases and
+                                              upsert_cases (the Chroma seam, ah_rag.collection)
 
 Stand-ins (test scaffolding, not product code):
   * encoder: sha1(text) seeds numpy.default_rng -> standard normal vector, L2-normalised in fp32
@@ -49,22 +52,42 @@ DIMS = {"all-MiniLM-L6-v2": 384, "sentence-transformers/all-MiniLM-L6-v2": 384}
 from oracle.encoder_stub import encode as stub_encode  # noqa: E402
 
 
+_TEXT_OF: dict = {}  # sha1 of an encoded single-text query vector -> its text (collection_cases)
+
+
+def _vsha(v) -> str:
+    return hashlib.sha1(np.asarray(v, np.float32).tobytes()).hexdigest()
+
+
 class StubSentenceTransformer:
     def __init__(self, model_name: str, **_):
         self.dim = DIMS.get(model_name, 384)
 
     def encode(self, texts, normalize_embeddings=False, show_progress_bar=False, **_):
-        return stub_encode(texts, self.dim, normalize=normalize_embeddings)
+        out = stub_encode(texts, self.dim, normalize=normalize_embeddings)
+        if not isinstance(texts, str) and len(texts) == 1 and normalize_embeddings:
+            _TEXT_OF[_vsha(out[0])] = texts[0]
+        return out
 
 
 _STORE: dict = {}
+# The raw collection traffic while RECORD["on"] (collection_cases.json): the reference's own
+# upsert / query arguments and the stand-in's answers, per collection (db directory name / name).
+RECORD: dict = {"on": False, "calls": []}
 
 
 class StubCollection:
-    def __init__(self):
+    def __init__(self, tag="", metadata=None):
         self.ids, self.vecs, self.metas, self.docs = [], [], [], []
+        self.tag, self.metadata = tag, metadata
 
     def upsert(self, ids, documents=None, embeddings=None, metadatas=None):
+        if RECORD["on"]:
+            # the vectors are the stand-in encoder's of the documents (checked): stored as text
+            enc = stub_encode(list(documents), len(embeddings[0]), normalize=True)
+            assert np.array_equal(enc, np.asarray(embeddings, np.float32)), "upsert vectors are not encode(documents)"
+            RECORD["calls"].append({"coll": self.tag, "op": "upsert", "ids": list(ids), "documents": list(documents),
+                                    "metadatas": [dict(m) for m in metadatas], "dim": len(embeddings[0])})
         for i, nid in enumerate(ids):
             vec = np.asarray(embeddings[i], np.float32)
             meta = dict(metadatas[i]) if metadatas else {}
@@ -86,6 +109,10 @@ class StubCollection:
             out["distances"].append([float(np.float32(1.0) - np.float32(s[i])) for i in order])
             out["metadatas"].append([self.metas[i] for i in order])
             out["documents"].append([self.docs[i] for i in order])
+        if RECORD["on"]:
+            RECORD["calls"].append({"coll": self.tag, "op": "query",
+                                    "texts": [_TEXT_OF[_vsha(q)] for q in query_embeddings],
+                                    "n_results": n_results, "include": list(include or []), "result": out})
         return out
 
 
@@ -94,10 +121,16 @@ class StubClient:
         self.path = os.path.abspath(path or ".")
 
     def delete_collection(self, name):
+        if RECORD["on"]:
+            RECORD["calls"].append({"coll": f"{os.path.basename(self.path)}/{name}", "op": "delete"})
         _STORE.pop((self.path, name), None)
 
     def get_or_create_collection(self, name, metadata=None):
-        return _STORE.setdefault((self.path, name), StubCollection())
+        if (self.path, name) not in _STORE:
+            _STORE[(self.path, name)] = StubCollection(f"{os.path.basename(self.path)}/{name}", metadata)
+            if RECORD["on"]:
+                RECORD["calls"].append({"coll": _STORE[(self.path, name)].tag, "op": "create", "metadata": metadata})
+        return _STORE[(self.path, name)]
 
 
 def install_stubs() -> None:
@@ -215,6 +248,7 @@ def main() -> None:
         hg = HierarchicalGraph.load(gdir)  # the loaded graph is what every caller sees
         db = os.path.join(work, "vector_db")
         hg.G.graph["vector_index"]["db_path"] = db
+        RECORD["on"] = True
         hg.build_vector_index(db_path=db, layers={0, 1}, reset=True)
         hg.save(gdir)
         out_graph = os.path.join(HERE, "reference_graph")
@@ -277,6 +311,8 @@ def main() -> None:
         hg3.build_vector_index(db_path=db3, layers={0, 1}, upsert_only=True)
         after = dict(hg3.G.graph["vector_index"]["indexed_meta"])
         post = [{"query": q, "result": hg3.search(q, top_k=8, return_cluster=True, db_path=db3)} for q in probe]
+        RECORD["on"] = False
+        dump("collection_cases.json", {"dim": 384, "model": "all-MiniLM-L6-v2", "calls": RECORD["calls"]})
         dump("upsert_cases.json", {"edits": edits, "new_entity": {"name": "Entity Brand New", "id": new_eid,
                                                                   "summary": sids[2]},
                                    "indexed_meta_before": before, "indexed_meta_after": after,

@@ -59,6 +59,72 @@ def single_reset(env: AHRAGGymEnv, hg, query: str, qvec: np.ndarray):
     return env._finish_reset(obs)
 
 
+def reference_loop(hg, tmp: str, steps: int, n_envs: int = 4, budget_s: float = 3.0, seed: int = 20251003) -> dict:
+    """The reference's PPO environment loop unchanged in shape (scripts/train_ppo.py:25-26,
+    policy_ppo.py:145,163-205): `n_envs` environments built by AHRAGGymEnv(graph_dir=...) from a
+    saved graph directory, then rounds of {reset every env with its question (the encoder in the
+    loop: AHR_ENCODER=hash, no weights offline), step each env one after another with a random
+    valid action until done}. Construction times are reported per environment (the first loads the
+    graph; the rest share it and its device structures, HierarchicalGraph.load_shared); the first
+    round (device graph, index upload, kernels' first calls) is reported and not timed."""
+    gdir = os.path.join(tmp, "graph_ref")
+    vi = hg.G.graph["vector_index"]
+    model = vi.get("model")
+    vi["model"] = "all-mpnet-base-v2"  # a 768-wide name: the hash encoder then matches the corpus width
+    t0 = time.perf_counter()
+    try:
+        hg.save(gdir)
+    finally:
+        vi["model"] = model
+    save_s = time.perf_counter() - t0
+    prev = os.environ.get("AHR_ENCODER")
+    os.environ["AHR_ENCODER"] = "hash"
+    rng = np.random.default_rng(seed)
+    try:
+        ctor_s, envs = [], []
+        for _ in range(n_envs):
+            t = time.perf_counter()
+            envs.append(AHRAGGymEnv(graph_dir=gdir, max_steps=steps))
+            ctor_s.append(time.perf_counter() - t)
+
+        def one_round(r: int) -> int:
+            n = 0
+            for e, env in enumerate(envs):
+                env.reset(f"question {r}.{e} about the corpus")
+            n += len(envs)
+            for env in envs:
+                done, k = False, 0
+                while not done and k < steps:
+                    a = random_actions(rng, [env.get_action_mask()])[0]
+                    _, _, done, _ = env.step(a)
+                    n += 1
+                    k += 1
+            return n
+        t = time.perf_counter()
+        one_round(0)
+        torch.cuda.synchronize()
+        first_s = time.perf_counter() - t
+        n_steps, r, t = 0, 1, time.perf_counter()
+        while True:
+            n_steps += one_round(r)
+            r += 1
+            if time.perf_counter() - t >= budget_s:
+                break
+        dt = time.perf_counter() - t
+    finally:
+        if prev is None:
+            os.environ.pop("AHR_ENCODER", None)
+        else:
+            os.environ["AHR_ENCODER"] = prev
+    shared = all(env.env.hg is envs[0].env.hg for env in envs)
+    return {"env_steps_per_s": round(n_steps / dt, 1), "rounds": r - 1, "env_steps": n_steps,
+            "n_envs": n_envs, "ctor_s": [round(x, 4) for x in ctor_s], "first_round_s": round(first_s, 3),
+            "graph_save_s": round(save_s, 2), "graph_shared": shared,
+            "what": (f"AHRAGGymEnv(graph_dir=...) x {n_envs} from a saved graph directory, then rounds of reset-all + "
+                     "each env stepped to done one after another (policy_ppo.py:145,163-205), random valid actions, "
+                     "hash encoder for the reset queries, fp32 index; env steps = resets + steps")}
+
+
 def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: int = 1, total_envs=None,
             backend: str = "nccl", episodes: int = 5, cpu_baseline_fn=None) -> dict:
     """One rank's C5 measurement: build the graph, then a warm-up episode and `episodes` timed
@@ -150,6 +216,7 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
         for i in range(n_s):
             hg.search_batch([queries[i]], top_k=5, member_top_m=5, query_vectors=qv[i:i + 1])
         search_s = (time.perf_counter() - ts) / n_s
+    ref_loop = reference_loop(hg, tmp, steps) if rank == 0 and single > 0 else None
     cpu = None
     if rank == 0 and cpu_baseline_fn is not None:
         cpu = cpu_baseline_fn(hg, ids, vectors, qv, steps)
@@ -176,6 +243,7 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
             "what": "HierarchicalGraph.search_batch([q], top_k=5, return_cluster=False) wall time per "
                     "call at B = 1 with a precomputed query vector (the body of the drop-in search(); "
                     "fp32 index, 90k rows), 256 calls after 8 warm-up calls"},
+        "reference_loop": ref_loop,
         "cpu_baseline": cpu,
         "graph": {"nodes": hg.G.number_of_nodes(), "edges": hg.G.number_of_edges(), "indexed": len(ids)},
         "build_s": round(t_build, 1), "parallelism": f"replicas{world} (environments partitioned, no collective)",

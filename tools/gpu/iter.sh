@@ -1,0 +1,16 @@
+#!/bin/bash
+# One development iteration on a box: every -m gpu test, then the C5 env line alone.
+# usage: bash tools/gpu/iter.sh OUTDIR [pytest -k expr]
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=${1:-gpurun_out/iter}; mkdir -p $O
+K=${2:+-k "$2"}
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread $K > $O/gputests.log 2>&1 || { echo TESTS_FAILED; tail -40 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 400 python -u tools/bench_env.py --envs 1024 --episodes 3 > $O/bench_env.json 2> $O/bench_env.err || { echo ENV_FAIL; tail -20 $O/bench_env.err; exit 1; }
+python - $O/bench_env.json <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print({k: d.get(k) for k in ("vec_env_steps_per_s", "single_env_steps_per_s", "dropin_search_b1", "reference_loop", "device_host_split_rank0")})
+PY

@@ -73,7 +73,7 @@ def main() -> None:
     dur = durations(os.path.join(a.pmc_dir, "trace", "*", "*_kernel_stats.csv"))
     out = {"_method": ("FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction) + WRITE_SIZE KiB x 1024, "
                        "mean per launch, separate rocprofv3 --pmc passes; durations from --kernel-trace --stats"),
-           "_source": a.pmc_dir, "_workload": a.workload, "_batch": a.batch}
+           "_source": a.pmc_dir, "_workload": a.workload, "_batch": a.batch, "_dt": a.dt}
     for k in sorted(set(fetch) | set(write) | set(dur)):
         base = k.split("<")[0]
         if base not in ("topk_tile_kernel", "topk_tilelane_kernel", "topk_lane_kernel", "topk_qkv_kernel", "topk_t256_kernel",
