@@ -2,6 +2,8 @@
 #include "ahr_common.h"
 #include "ahr.h"
 
+#include <stdlib.h>
+
 #include <string>
 
 namespace ahr {
@@ -69,19 +71,25 @@ int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* q = static_cast<char*>(ws);
   char* a = q + ((int64_t)B * dim * 4 + 255) / 256 * 256;
-  AHR_HIP(hipMemcpyAsync(q, host_q, (size_t)B * dim * 4, hipMemcpyHostToDevice, s));
+  // AHR_SEARCH_SKIP (diagnostic cost split, wrong results): bit 0 skips the query copy, bit 1 the
+  // result copy, bit 2 the rerank launch
+  static const int skip = [] {
+    const char* e = getenv("AHR_SEARCH_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  if (!(skip & 1)) AHR_HIP(hipMemcpyAsync(q, host_q, (size_t)B * dim * 4, hipMemcpyHostToDevice, s));
   float* scores = reinterpret_cast<float*>(a + off[0]);
   int32_t* rows = reinterpret_cast<int32_t*>(a + off[1]);
   st = ahr_index_query(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream);
   if (st != AHR_OK) return st;
-  st = ahr_graph_expand_rerank_rows(g, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp,
+  if (!(skip & 4)) st = ahr_graph_expand_rerank_rows(g, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp,
                                     reinterpret_cast<int32_t*>(a + off[2]), reinterpret_cast<double*>(a + off[3]),
                                     reinterpret_cast<int32_t*>(a + off[4]), reinterpret_cast<int32_t*>(a + off[5]),
                                     reinterpret_cast<int32_t*>(a + off[6]), reinterpret_cast<double*>(a + off[7]),
                                     reinterpret_cast<double*>(a + off[8]), reinterpret_cast<int32_t*>(a + off[9]),
                                     stream);
   if (st != AHR_OK) return st;
-  AHR_HIP(hipMemcpyAsync(host_out, a, (size_t)arena, hipMemcpyDeviceToHost, s));
+  if (!(skip & 2)) AHR_HIP(hipMemcpyAsync(host_out, a, (size_t)arena, hipMemcpyDeviceToHost, s));
   AHR_HIP(hipStreamSynchronize(s));
   return AHR_OK;
 }

@@ -2344,7 +2344,7 @@ __device__ __forceinline__ void convert_row_fast(const float* __restrict__ x, in
     }
     *reinterpret_cast<uint2*>(row + 2 * (int64_t)j) = w;
     if (frag) {  // the 4 elements stay inside one 16-B chunk of the fragment-major copy
-      const int64_t o = (((q >> 5) * (d_pad >> 4) + (j >> 4)) * 64 + (q & 31) + 32 * ((j >> 3) & 1)) * 16 + (j & 7) * 2;
+      const int64_t o = qres::frag_chunk(q, j, d_pad >> 4) * 16 + (j & 7) * 2;
       *reinterpret_cast<uint2*>(frag + o) = w;
     }
   }
@@ -2367,8 +2367,8 @@ __global__ __launch_bounds__(256) void convert_queries_frag_kernel(const float* 
 
 // The register-resident plan's fragment-major query copy straight from the fp32 queries, when
 // nothing else reads the row-major copy (self-seeded launches: no pre-pass) and the rows need no
-// normalisation: one thread per 16-B chunk of the copy (query 32 g + l % 32, dims 16 S + 8 (l / 32)
-// .. + 8, the convert kernel's rounding), so a wave writes one contiguous KiB. The row-major
+// normalisation: one thread per 16-B chunk of the copy (qres::frag_elem: its query and 8 elements,
+// the convert kernel's rounding), so a wave writes one contiguous KiB. The row-major
 // convert wrote each 16-B chunk as two 8-B pieces 1 KiB apart, plus the unused rows.
 __global__ __launch_bounds__(256) void frag_from_f32_kernel(const float* __restrict__ src, int64_t n, int dim, int d_pad,
                                                             int dt, int64_t n16, uint8_t* __restrict__ frag,
@@ -2376,12 +2376,9 @@ __global__ __launch_bounds__(256) void frag_from_f32_kernel(const float* __restr
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i == 0 && epoch) advance_epoch_rebalance(epoch);  // the next qres launch's tag
   if (i >= n16) return;
-  const int l = (int)(i & 63);
-  const int ns = d_pad >> 4;
-  const int64_t gs = i >> 6;
-  const int S = (int)(gs % ns);
-  const int64_t q = (gs / ns) * 32 + (l & 31);
-  const int j0 = 16 * S + 8 * (l >> 5);
+  int64_t q;
+  int j0;
+  qres::frag_elem(i, d_pad >> 4, &q, &j0);
   float v[8];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {

@@ -217,6 +217,17 @@ __device__ __forceinline__ void mfma_step(const u32x4& a, const u32x4& b, f32x16
   }
 }
 
+// one v_mfma_f32_16x16x32 (bf16 / f16) step: acc + a . b (the t256 / small kernels' fragment map)
+template <int DT>
+__device__ __forceinline__ f32x4 mfma16_step(const u32x4& a, const u32x4& b, const f32x4& acc) {
+  if constexpr (DT == DT_BF16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
+                                                   0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc,
+                                                  0, 0, 0);
+}
+
 // Runtime-indexed read of a register list without scratch: a select chain. The opaque copy
 // of j stops LLVM from folding the chain back into an indexed load (which would demote the
 // whole list to scratch memory).

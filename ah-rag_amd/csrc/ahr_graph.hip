@@ -19,6 +19,7 @@
 #include "ahr.h"
 
 #include <math.h>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -166,28 +167,203 @@ __global__ __launch_bounds__(64) void expand_rerank_kernel(
   out_count[q] = m;
 }
 
+// The same pass with one wave per query and every step parallel over the wave (the default when a
+// query's candidates fit kWaveCand): the serial kernel above chains ~30 dependent global loads per
+// query and re-reads its own growing dict from memory for every membership test (45 us of the
+// drop-in B = 1 search). Here the dict is rebuilt from its definition instead of by insertion:
+//   * candidates, in the reference's order (:727-740): per seed s (lane s) the seed itself, then its
+//     first `lim` belongs_to parents (entity) / members (summary), laid out by a wave prefix sum of
+//     the per-seed counts, all loads of a level issued together;
+//   * the dict: a node's position is its first candidate, its value the LAST seed candidate of that
+//     node if it has one (a seed assignment overwrites in place), else its first candidate (an
+//     expansion only adds an absent id) — exactly the insertion semantics;
+//   * rerank (:743-782): each entry's score with the same left-to-right double arithmetic; the
+//     stable descending sort on the rounded score is a rank: #{kept j: rs_j > rs_i} + #{kept j < i:
+//     rs_j == rs_i}; ranks below top_k are written.
+// Bitwise equal to expand_rerank_kernel (tests/test_dropin_gpu.py, test_rerank_rounding.py).
+constexpr int kWaveCand = 1024;  // candidates (and dict entries) per query held in LDS
+constexpr int kWaveSeeds = 64;   // one seed per lane
+
+__global__ __launch_bounds__(64) void expand_rerank_wave_kernel(
+    DevGraph g, const int32_t* __restrict__ seed_nodes, const int32_t* __restrict__ row_map, int64_t n_map,
+    const float* __restrict__ seed_sem, int B, int k_seed, ahr_rerank_params p, int max_exp,
+    int32_t* __restrict__ exp_nodes, double* __restrict__ exp_sem, int32_t* __restrict__ exp_src,
+    int32_t* __restrict__ exp_count, int32_t* __restrict__ out_nodes, double* __restrict__ out_sem,
+    double* __restrict__ out_score, int32_t* __restrict__ out_count) {
+  __shared__ int32_t c_node[kWaveCand];
+  __shared__ int32_t c_src[kWaveCand];  // seed index (>= 0) or -1 - assumed node type (expansion)
+  __shared__ double c_sem[kWaveCand];
+  __shared__ int32_t e_node[kWaveCand];
+  __shared__ double e_sem[kWaveCand];
+  __shared__ double e_rs[kWaveCand];  // rounded score
+  __shared__ uint8_t e_keep[kWaveCand];  // passed the filters
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (q >= B) return;
+
+  // ---- candidates: lane s owns seed s
+  int32_t nid = -1;
+  double sem = 0.0;
+  int adj = 0, cnt_exp = 0, code = 0;
+  double factor = 0.0;
+  int64_t b0 = 0;
+  if (lane < k_seed) {
+    nid = seed_nodes[(int64_t)q * k_seed + lane];
+    if (row_map) nid = nid >= 0 && nid < n_map ? row_map[nid] : -1;
+    const float dist = 1.0f - seed_sem[(int64_t)q * k_seed + lane];  // Chroma's float32 distance
+    sem = 1.0 - (double)dist;
+    if (nid >= 0 && nid < g.n_nodes) {
+      const int8_t t = g.type[nid];
+      int lim = 0;
+      if (t == AHR_NODE_ENTITY) {
+        adj = ADJ_BT_OUT; lim = 2; factor = 0.9; code = -1 - AHR_NODE_SUMMARY;
+      } else if (t == AHR_NODE_SUMMARY) {
+        adj = ADJ_BT_IN; lim = p.member_top_m; factor = 0.85; code = -1 - AHR_NODE_ENTITY;
+      }
+      if (lim > 0) {
+        b0 = g.off[adj][nid];
+        const int64_t deg = g.off[adj][nid + 1] - b0;
+        cnt_exp = (int)(deg < lim ? deg : lim);
+      }
+    }
+  }
+  const int cnt = nid >= 0 ? 1 + cnt_exp : 0;
+  // exclusive prefix sum of cnt over the wave
+  int incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  const int total = __shfl(incl, 63, 64);
+  const int pre = incl - cnt;
+  if (cnt) {
+    c_node[pre] = nid;
+    c_sem[pre] = sem;
+    c_src[pre] = lane;
+    const double es = sem * factor;
+    for (int j = 0; j < cnt_exp; ++j) {
+      c_node[pre + 1 + j] = g.tgt[adj][b0 + j];
+      c_sem[pre + 1 + j] = es;
+      c_src[pre + 1 + j] = code;
+    }
+  }
+  __syncthreads();
+
+  // ---- the dict: first occurrences in candidate order, values from the last seed occurrence
+  int n = 0;
+  for (int base = 0; base < total; base += 64) {
+    const int i = base + lane;
+    bool first = false;
+    int val = i;
+    if (i < total) {
+      const int32_t v = c_node[i];
+      first = true;
+      int last_seed = -1;
+      for (int j = 0; j < total; ++j) {
+        if (c_node[j] == v) {
+          if (j < i) first = false;
+          if (c_src[j] >= 0) last_seed = j;
+        }
+      }
+      if (last_seed >= 0) val = last_seed;
+    }
+    const uint64_t m = __ballot(first);
+    const int idx = n + __popcll(m & ((1ull << lane) - 1));
+    if (first) {
+      const int32_t v = c_node[i];
+      e_node[idx] = v;
+      e_sem[idx] = c_sem[val];
+      exp_nodes[(int64_t)q * max_exp + idx] = v;
+      exp_sem[(int64_t)q * max_exp + idx] = c_sem[val];
+      exp_src[(int64_t)q * max_exp + idx] = c_src[val];
+    }
+    n += __popcll(m);
+  }
+  if (lane == 0) exp_count[q] = n;
+  if (p.top_k <= 0) {
+    if (lane == 0) out_count[q] = 0;
+    return;
+  }
+  __syncthreads();
+
+  // ---- rerank: scores and filters per entry (hierarchical_graph.py:743-779)
+  for (int i = lane; i < n; i += 64) {
+    const int32_t v = e_node[i];
+    const bool known = v < g.n_nodes;
+    const int t = known ? g.type[v] : AHR_NODE_OTHER;
+    const double judge = known ? g.judge[v] : NAN;
+    const double conf = known ? g.conf[v] : NAN;
+    bool keep = true;
+    if (p.type_mask && !((p.type_mask >> t) & 1)) keep = false;
+    if (!isnan(p.judge_min) && (isnan(judge) || judge < p.judge_min)) keep = false;
+    if (!isnan(p.confidence_min) && (isnan(conf) || conf < p.confidence_min)) keep = false;
+    const double jt = (known && !isnan(judge)) ? g.judge_term[v] : 0.0;
+    const double ct = (known && !isnan(conf)) ? g.conf_term[v] : 0.0;
+    const double s = e_sem[i];
+    double score = p.alpha * s;  // left-to-right, every operation rounded (:768)
+    score = score + p.beta * jt;
+    score = score + p.gamma * ct;
+    score = score + p.delta * p.layer_boost[t];
+    e_rs[i] = py_round4(score);
+    e_keep[i] = keep;
+  }
+  __syncthreads();
+  // ---- stable sort descending on the rounded score, [:top_k] (:781-782), as ranks
+  int kept = 0;
+  for (int i = lane; i < n; i += 64) {
+    if (!e_keep[i]) continue;
+    const double rs = e_rs[i];
+    ++kept;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+      const double o = e_rs[j];
+      rank += (e_keep[j] && (o > rs || (j < i && o == rs))) ? 1 : 0;
+    }
+    if (rank < p.top_k) {
+      out_nodes[(int64_t)q * p.top_k + rank] = e_node[i];
+      out_sem[(int64_t)q * p.top_k + rank] = py_round4(e_sem[i]);
+      out_score[(int64_t)q * p.top_k + rank] = rs;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) kept += __shfl_xor(kept, d, 64);
+  if (lane == 0) out_count[q] = kept < p.top_k ? kept : p.top_k;
+}
+
 // GraphEnvironment expansions. Streams the reference's raw neighbour sequence but keeps only
 // the first `limit` distinct ids: that prefix is all that survives dict.fromkeys()[:limit],
 // and the per-input break (raw length >= limit after an input node) is tracked on the raw count.
 struct Emit {
-  int32_t* out;
+  int32_t* out;   // the kept ids: out[i * stride]
+  int stride;
   int limit;
   int n;       // distinct ids kept
   int64_t raw; // raw appends (the reference's len(expanded) before dedupe)
   __device__ bool full() const { return n >= limit; }
   __device__ void push(int32_t v) {
     ++raw;
-    if (n < limit && !has_entry(out, n, v)) out[n++] = v;
+    if (n >= limit) return;
+    for (int i = 0; i < n; ++i)
+      if (out[i * stride] == v) return;
+    out[n++ * stride] = v;
   }
 };
 
+// The kept ids live in LDS while the walk dedupes against them (interleaved per thread: entry i of
+// thread t at i * 64 + t, conflict-free) for limits up to kExpLds, else in the output row itself
+// (every membership test then an L2 round trip).
+constexpr int kExpLds = 32;
+
+template <bool kLds>
 __global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
                                                     const int32_t* __restrict__ inputs, int B,
                                                     int n_in, int limit, int32_t* __restrict__ out,
                                                     int32_t* __restrict__ out_count) {
+  __shared__ int32_t sbuf[kLds ? kExpLds * 64 : 1];
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= B) return;
-  Emit em{out + (int64_t)q * limit, limit, 0, 0};
+  Emit em{kLds ? sbuf + threadIdx.x : out + (int64_t)q * limit, kLds ? 64 : 1, limit, 0, 0};
   for (int i = 0; i < n_in && !em.full(); ++i) {
     const int32_t nid = inputs[(int64_t)q * n_in + i];
     if (nid < 0 || nid >= g.n_nodes) continue;  // `if nid not in self.hg.G: continue`
@@ -215,7 +391,20 @@ __global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
     }
     if (em.raw >= limit) break;  // `if len(expanded) >= limit: break`
   }
+  if constexpr (kLds)
+    for (int i = 0; i < em.n; ++i) out[(int64_t)q * limit + i] = sbuf[i * 64 + threadIdx.x];
   out_count[q] = em.n;
+}
+
+// launch on B queries (one thread each)
+inline void launch_expand(hipStream_t s, const DevGraph& dg, int action, const int32_t* inputs, int B, int n_in,
+                          int limit, int32_t* out, int32_t* out_count) {
+  if (limit <= kExpLds)
+    hipLaunchKernelGGL(expand_kernel<true>, dim3((B + 63) / 64), dim3(64), 0, s, dg, action, inputs, B, n_in, limit,
+                       out, out_count);
+  else
+    hipLaunchKernelGGL(expand_kernel<false>, dim3((B + 63) / 64), dim3(64), 0, s, dg, action, inputs, B, n_in, limit,
+                       out, out_count);
 }
 
 // expand_to_lca (environment.py:243-299): per query, the intersection over its input nodes of
@@ -602,10 +791,24 @@ static int expand_rerank_impl(ahr_graph* g, const int32_t* seed_nodes, const int
     return fail(AHR_EINVAL, "null buffer");
   const ahr_rerank_params p = *params;
   DeviceGuardG dg(g->device);
-  hipLaunchKernelGGL(expand_rerank_kernel, dim3((B + 63) / 64), dim3(64), 0,
-                     reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
-                     k_seed, p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
-                     out_score, out_count);
+  // one wave per query while its candidates fit the wave kernel's LDS (every search() / env reset
+  // shape: k_seed <= 64); the serial kernel otherwise (large top_k). AHR_RERANK_SERIAL=1: always the
+  // serial kernel (A/B; both are bitwise equal).
+  static const bool serial_only = [] {
+    const char* e = getenv("AHR_RERANK_SERIAL");
+    return e && atoi(e) != 0;
+  }();
+  const int lim_max = fan > 2 ? fan : 2;
+  if (!serial_only && k_seed <= kWaveSeeds && (int64_t)k_seed * (1 + lim_max) <= kWaveCand)
+    hipLaunchKernelGGL(expand_rerank_wave_kernel, dim3((unsigned)B), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
+                       k_seed, p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
+                       out_score, out_count);
+  else
+    hipLaunchKernelGGL(expand_rerank_kernel, dim3((B + 63) / 64), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
+                       k_seed, p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
+                       out_score, out_count);
   AHR_HIP(hipGetLastError());
   return AHR_OK;
 }
@@ -637,9 +840,7 @@ int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int
   if (B == 0) return AHR_OK;
   if ((n_in > 0 && !inputs) || !out_count || (limit > 0 && !out)) return fail(AHR_EINVAL, "null buffer");
   DeviceGuardG dg(g->device);
-  hipLaunchKernelGGL(expand_kernel, dim3((B + 63) / 64), dim3(64), 0,
-                     reinterpret_cast<hipStream_t>(stream), g->dg, action, inputs, B, n_in, limit,
-                     out, out_count);
+  launch_expand(reinterpret_cast<hipStream_t>(stream), g->dg, action, inputs, B, n_in, limit, out, out_count);
   AHR_HIP(hipGetLastError());
   return AHR_OK;
 }
@@ -673,8 +874,7 @@ int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, 
   int32_t* d_out = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + al((int64_t)B * n_in * 4));
   int32_t* d_cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d_out) + al((int64_t)B * lim * 4));
   if (n_in > 0) AHR_HIP(hipMemcpyAsync(d_in, host_inputs, (size_t)B * n_in * 4, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(expand_kernel, dim3((B + 63) / 64), dim3(64), 0, s, g->dg, action, d_in, B, n_in, limit,
-                     d_out, d_cnt);
+  launch_expand(s, g->dg, action, d_in, B, n_in, limit, d_out, d_cnt);
   AHR_HIP(hipGetLastError());
   // out and count are adjacent (count after out's padded part): one copy when out needs no padding
   if ((int64_t)B * lim * 4 == al((int64_t)B * lim * 4) && host_count == host_out + (int64_t)B * lim) {

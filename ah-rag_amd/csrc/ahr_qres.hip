@@ -72,6 +72,7 @@ struct Cfg {
   static_assert(kPieces % kWaves == 0, "equal DMA share per wave");
   static constexpr int kPPW = kPieces / kWaves;   // pieces per wave per stage
   static constexpr int kNS = NKT * 4;             // k16 steps = query fragments per lane
+  static constexpr bool kMma16 = mma16_for(kNS);  // the block product's MFMA shape (ahr_qres.h)
   static constexpr int kSS = kSK * 4;             // k16 steps per block
   // LDS: the ring, the lane buffers, the landing zones, the event table
   static constexpr int kOffBuf = kSlots * kStage;
@@ -147,11 +148,10 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t* __restrict__ q
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one 16-B chunk of the output
   if (i == 0 && epoch) advance_epoch_rebalance(epoch);
   if (i >= n16) return;
-  const int l = (int)(i & 63);
-  const int64_t gs = i >> 6;
-  const int S = (int)(gs % ns);
-  const int64_t q = (gs / ns) * 32 + (l & 31);
-  const u32x4 v = *reinterpret_cast<const u32x4*>(qbuf + q * row_stride + S * 32 + (l >> 5) * 16);
+  int64_t q;
+  int j0;
+  frag_elem(i, ns, &q, &j0);  // (2-byte elements)
+  const u32x4 v = *reinterpret_cast<const u32x4*>(qbuf + q * row_stride + 2 * j0);
   *reinterpret_cast<u32x4*>(qfrag + i * 16) = v;
 }
 
@@ -342,7 +342,11 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     }
     thr = fmaxf(thr, key_score(mn));
   };
-  // the rows of score e of quad qd: r0 + 8 qd + 4 fh + e. A passing quad's scores are tested one by
+  // the block row of score e of quad qd (acc[4 qd + e]): quad_row(qd) + e
+  auto quad_row = [&](int qd) __attribute__((always_inline)) {
+    return C::kMma16 ? 16 * (qd >> 1) + 8 * fh + 4 * (qd & 1) : 8 * qd + 4 * fh;
+  };
+  // the rows of score e of quad qd: r0 + quad_row(qd) + e. A passing quad's scores are tested one by
   // one, each passing score one append; a quad compacts first when its 4 possible appends might
   // not fit.
   auto screen_quad = [&](float v0, float v1, float v2, float v3, int qrow, bool ragged) __attribute__((always_inline)) {
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
         bm = -INFINITY;
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-          if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) bm = fmaxf(bm, acc[j]);
+          if (r0 + quad_row(j >> 2) + (j & 3) < n_rows) bm = fmaxf(bm, acc[j]);
       }
       rmo = max(rmo, ord_f32(bm) | 1u);  // a new maximum is marked risen
     }
@@ -384,7 +388,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
       if (qm[qd] >= thr) screen_quad(acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3],
-                                     r0 + 8 * qd + 4 * fh, ragged);
+                                     r0 + quad_row(qd), ragged);
   };
 
   // ---- self-seeding (see the header) ----
@@ -568,7 +572,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       const uint64_t a = lbuf[(kPark + 2 * qd) * kThreads], b = lbuf[(kPark + 1 + 2 * qd) * kThreads];
       const float v0 = __uint_as_float((uint32_t)a), v1 = __uint_as_float((uint32_t)(a >> 32));
       const float v2 = __uint_as_float((uint32_t)b), v3 = __uint_as_float((uint32_t)(b >> 32));
-      if (fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)) >= thr) screen_quad(v0, v1, v2, v3, r0 + 8 * qd + 4 * fh, ragged);
+      if (fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)) >= thr) screen_quad(v0, v1, v2, v3, r0 + quad_row(qd), ragged);
     }
   };
 
@@ -585,10 +589,17 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // per-lane values (the four precomputed offsets would cost two more live registers).
   // The four per-lane chunk offsets (s % 4 = m: a_row + 32 (m ^ h) + 16 (fh ^ a0)) are kept in
   // registers, so a read costs one v_add (the slot base) and an immediate k-tile offset.
+  // 16x16x32 (kMma16): fragment m = 2 s2 + r of a k-tile is the 32-deep step s2's row subtile r:
+  // row 16 r + l % 16, logical chunk 4 s2 + l / 16 (the same 16 B per lane and instruction).
   int a_off[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    a_off[m] = fr * kRowBytes + ((((2 * m + fh) ^ ((fr >> 1) & 7))) << 4);
+    if constexpr (C::kMma16) {
+      const int row = 16 * (m & 1) + (lane & 15);
+      a_off[m] = row * kRowBytes + (((4 * (m >> 1) + (lane >> 4)) ^ ((row >> 1) & 7)) << 4);
+    } else {
+      a_off[m] = fr * kRowBytes + ((((2 * m + fh) ^ ((fr >> 1) & 7))) << 4);
+    }
     asm volatile("" : "+v"(a_off[m]));  // materialized once, here
   }
   auto frag = [&](int st, int s, int h = 0) __attribute__((always_inline)) {  // h: the stage's block
@@ -600,20 +611,54 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   constexpr bool skip_screen = (ABL & ABL_NOSCREEN) != 0;
   f32x16 acc;
   u32x4 fa[3];
-  // a block's kSS k16 steps: step t prefetches step t + 2 and multiplies step t
+  // a block's kSS fragments: fragment t prefetches fragment t + 2 and is multiplied.
+  // 32x32x16: fragment t = k16 step t, one MFMA. 16x16x32: fragment t = (32-deep step t / 2, row
+  // subtile r = t % 2), two MFMAs (query tiles 0 and 1: c[2 r] and c[2 r + 1]); after the chain one
+  // v_permlane16_swap per register pair gives each lane the 32x32 form's share — one query (lane %
+  // 32) and 16 rows — so the screening below is the same code (quad rows: quad_row).
   auto stage_mma = [&](int st, int h = 0) __attribute__((always_inline)) {
+    if constexpr (C::kMma16) {
+      f32x4 c[4];
 #pragma unroll
-    for (int t = 0; t < C::kSS; ++t) {
-      if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2, h);
-      __builtin_amdgcn_sched_barrier(0);
-      if (t == 0) {
-        f32x16 z = {};
-        mfma_step<DT>(fa[0], qf[0], z);
-        acc = z;
-      } else {
-        mfma_step<DT>(fa[t % 3], qf[t], acc);
+      for (int t = 0; t < C::kSS; ++t) {
+        if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2, h);
+        __builtin_amdgcn_sched_barrier(0);
+        const int r = t & 1;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const f32x4 prev = t < 2 ? f32x4{} : c[2 * r + qt];
+          c[2 * r + qt] = mfma16_step<DT>(fa[t % 3], qf[2 * (t >> 1) + qt], prev);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      // lane (R = l / 16, c = l % 16) held query c (c[2 r]) and 16 + c (c[2 r + 1]), rows 16 r + 4 R
+      // + e; the swap moves query 16 + c to the odd rows R and query c to the even ones, so lane l
+      // holds query l % 32: c[2 r] rows 16 r + 8 (l / 32) + e, c[2 r + 1] the 4 rows after them
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto w = __builtin_amdgcn_permlane16_swap(__float_as_uint(c[2 * r][e]),
+                                                          __float_as_uint(c[2 * r + 1][e]), false, false);
+          c[2 * r][e] = __uint_as_float(w[0]);
+          c[2 * r + 1][e] = __uint_as_float(w[1]);
+        }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = c[i >> 2][i & 3];
+    } else {
+#pragma unroll
+      for (int t = 0; t < C::kSS; ++t) {
+        if (t + 2 < C::kSS) fa[(t + 2) % 3] = frag(st, t + 2, h);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t == 0) {
+          f32x16 z = {};
+          mfma_step<DT>(fa[0], qf[0], z);
+          acc = z;
+        } else {
+          mfma_step<DT>(fa[t % 3], qf[t], acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   auto finish_block = [&](int bi) __attribute__((always_inline)) {  // bi: the block just multiplied
@@ -627,7 +672,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
       float bm = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 16; ++j)  // block 0 is never ragged (>= 2 blocks per split) but check anyway
-        if (r0 + 8 * (j >> 2) + 4 * fh + (j & 3) < n_rows) bm = fmaxf(bm, acc[j]);
+        if (r0 + quad_row(j >> 2) + (j & 3) < n_rows) bm = fmaxf(bm, acc[j]);
       rmo = max(rmo, ord_f32(bm) | 1u);
       publish();
       return;

@@ -1,8 +1,10 @@
 """The 256-query register-resident kernel (csrc/ahr_qres.hip) — the default B >= 512 bf16/f16 plan at
 d = 768 and 384, k <= 12 (the C2 headline shape; reference src/ah_rag/graph/hierarchical_graph.py:714).
 
-It chains the MFMA steps of the lane-local tile kernel (topk_tilelane_kernel) in the same k order,
-so scores AND rows must be bitwise equal to it — with its admission threshold seeded by itself
+At d = 768 its block product is a chain of v_mfma_f32_16x16x32 over 32-deep steps in k order, the
+chain of the 256x256 tile kernel (topk_t256_kernel); at d = 384 the 32x32x16 chain of the lane-local
+tile kernel (topk_tilelane_kernel); scores AND rows must be bitwise equal to that reference (ref_of)
+— with its admission threshold seeded by itself
 (the default: splits publish per-query maxima, the k-th largest becomes the seed), by the sampled
 pre-pass launch (flag 1 << 26), or not at all (sample rows 0: every score a candidate, the survivor
 buffers' compaction path) — including ragged row and query blocks, splits with no rows, adversarial
@@ -27,6 +29,13 @@ MUTE = 4            # split 0 seeds under a tag no launch has: every bounded wai
 T256 = 32768        # the 256x256 16x16x32 tile kernel
 
 
+def ref_of(d):
+    """The bitwise reference of the register-resident kernel at width d (ahr_qres.h AHR_QRES_MMA16 = 1,
+    the shipped build): at d = 768 its block product is a chain of v_mfma_f32_16x16x32 over 32-deep
+    steps in k order, the t256 kernel's chain; at d = 384 the 32x32x16 chain of the tilelane kernel."""
+    return (T256, "t256") if d > 384 else (TILELANE, "tilelane128")
+
+
 def _clustered(rng, n, d, n_centers=50, noise=0.35):
     c = dr.normalize_rows(rng.standard_normal((n_centers, d)).astype(np.float32))
     lab = rng.integers(0, n_centers, n)
@@ -46,7 +55,7 @@ def _check_forms(ix, Q, k):
     """Self-seeded and pre-pass-seeded launches against the tile kernel, bitwise; returns the
     self-seeded (default) result."""
     a = _run(ix, Q, k, QRES, "qres256")
-    d = _run(ix, Q, k, TILELANE, "tilelane128")
+    d = _run(ix, Q, k, *ref_of(ix.dim))
     np.testing.assert_array_equal(a[1], d[1])
     np.testing.assert_array_equal(a[0], d[0])
     e = _run(ix, Q, k, QRES | PREPASS, "qres256")
@@ -171,7 +180,7 @@ def test_qres_xcd_balanced_splits(cuda):
     Q = _clustered(rng, 1024, 768)
     ix = DenseIndex(768, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
-    ref = _run(ix, Q, 10, TILELANE, "tilelane128")
+    ref = _run(ix, Q, 10, *ref_of(ix.dim))
     for _ in range(6):
         s, r = _run(ix, Q, 10, QRES | (1 << 28), "qres256")
         np.testing.assert_array_equal(r, ref[1])
@@ -185,7 +194,9 @@ def test_qres_compaction_below_k(cuda, prepass):
     keys would exceed the lane's k-th best and drop the 12th. Query 0's 11 best rows all sit in one
     lane's rows of one block (the lane's 16 rows of a 32-row block are block offsets 0-3, 8-11,
     16-19, 24-27; 19 and 24-27 score low, so the next quad starts with 11 buffered keys and
-    compacts), its 12th best in the same lane one block later; the split's other rows score -1."""
+    compacts), its 12th best in the same lane one block later; the split's other rows score -1.
+    (That is the 32x32x16 form's lane map; the 16x16x32 form's lane fh = 0 holds block offsets 0-7
+    and 16-23 in quads 0-3, 4-7, 16-19, 20-23: there rows 19 and 20-23 score low.)"""
     from ah_rag.embeddings import DenseIndex
     rng = np.random.default_rng(71)
     d, n, k = 768, 40000, 12
@@ -201,7 +212,8 @@ def test_qres_compaction_below_k(cuda, prepass):
 
     base = 39520  # block 5 of the last split (64 splits of 1,250 row blocks: rows 39,360..)
     C[39360:] = -q0  # nothing else of that split enters the lane's buffer
-    for i, off in enumerate((0, 1, 2, 3, 8, 9, 10, 11, 16, 17, 18)):
+    offs = (0, 1, 2, 3, 4, 5, 6, 7, 16, 17, 18) if ref_of(d)[0] == T256 else (0, 1, 2, 3, 8, 9, 10, 11, 16, 17, 18)
+    for i, off in enumerate(offs):
         C[base + off] = at(0.99 - 0.01 * i)
     C[base + 32] = at(0.85)
     ix = DenseIndex(d, n, dtype="bf16", device=cuda)
@@ -209,7 +221,7 @@ def test_qres_compaction_below_k(cuda, prepass):
     flags = QRES | (PREPASS if prepass else 0)
     s, r = _run(ix, Q, k, flags, "qres256")
     assert r[0, k - 1] == base + 32, r[0]
-    d_ = _run(ix, Q, k, TILELANE, "tilelane128")
+    d_ = _run(ix, Q, k, *ref_of(ix.dim))
     np.testing.assert_array_equal(r, d_[1])
     np.testing.assert_array_equal(s, d_[0])
     ix.close()
@@ -281,7 +293,7 @@ def test_qres_query_conversion_paths(cuda, dim, normalize):
     ix = DenseIndex(dim, len(C), dtype="bf16", device=cuda)
     ix.upsert(C)
     outs = []
-    for flags, kernel in ((QRES, "qres256"), (TILELANE, "tilelane128")):
+    for flags, kernel in ((QRES, "qres256"), ref_of(ix.dim)):
         ix.set_debug_flags(flags)
         assert ix.plan(len(Q), 10)["kernel"] == kernel
         outs.append([t.cpu().numpy() for t in ix.query(Q, 10, normalize=normalize)])
@@ -303,7 +315,7 @@ def test_qres_consecutive_launches(cuda):
     Qs = [_clustered(rng, B, 768) for B, _ in shapes]
     ix.set_debug_flags(QRES)
     got = [[t.cpu().numpy() for t in ix.query(Q, k)] for Q, (_, k) in zip(Qs, shapes)]
-    ix.set_debug_flags(TILELANE)
+    ix.set_debug_flags(ref_of(ix.dim)[0])
     for Q, (_, k), a in zip(Qs, shapes, got):
         b = [t.cpu().numpy() for t in ix.query(Q, k)]
         np.testing.assert_array_equal(a[1], b[1])
@@ -349,7 +361,7 @@ def test_qres_seed_wait_timeouts(cuda, d, n, B, k):
     Q = _clustered(rng, B, d)
     ix = DenseIndex(d, n, dtype="bf16", device=cuda)
     ix.upsert(C)
-    ref = _run(ix, Q, k, TILELANE, "tilelane128")
+    ref = _run(ix, Q, k, *ref_of(ix.dim))
     for flags in (QRES | MUTE, QRES, QRES | MUTE, QRES | MUTE):
         s, r = _run(ix, Q, k, flags, "qres256")
         np.testing.assert_array_equal(r, ref[1])

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--envs", type=int, default=64)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--search", action="store_true")
+    ap.add_argument("--raw", action="store_true",
+                    help="with --search: also time SearchEngine.run and the bare ahr_search_host call (the floor)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(7)
@@ -64,6 +66,28 @@ def main():
     prof.disable()
     if a.search:
         print(f"search_batch B = 1: {a.envs / wall:.1f} calls/s ({wall / a.envs * 1e3:.4f} ms per call)", flush=True)
+        if a.raw:
+            from ah_rag import _native as nat
+            from ah_rag.graph_search import resolve_search_params
+            eng = hg.search_engine(hg.G.graph["vector_index"]["db_path"])
+            params = resolve_search_params(hg.G.graph.get("search_params", {}), 5, 5, *([None] * 7))
+            qt = torch.from_numpy(qv[:1].copy())
+            eng.run(qt, params)
+            t0 = time.perf_counter()
+            for _ in range(a.envs):
+                eng.run(qt, params)
+            print(f"SearchEngine.run B = 1: {(time.perf_counter() - t0) / a.envs * 1e3:.4f} ms per call", flush=True)
+            (key, b), = [(k, v) for k, v in eng._hbufs.items() if k[0] == 1]
+            ws, ws_bytes, q_host, q_np, out, views = b
+            c = params.to_c_cached()
+            args = (eng.index.handle, eng.graph._h, q_host.data_ptr(), 1, key[2], eng.row_to_node.data_ptr(),
+                    int(eng.row_to_node.shape[0]), nat.ctypes.byref(c), key[3], ws.data_ptr(), ws_bytes,
+                    out.data_ptr(), nat.stream_ptr())
+            fn = nat.lib().ahr_search_host
+            t0 = time.perf_counter()
+            for _ in range(a.envs):
+                fn(*args)
+            print(f"bare ahr_search_host B = 1: {(time.perf_counter() - t0) / a.envs * 1e3:.4f} ms per call", flush=True)
     else:
         print(f"single env: {a.envs * (1 + a.steps) / wall:.1f} env-steps/s "
               f"({wall / a.envs * 1e3:.3f} ms per episode of reset + {a.steps} steps)", flush=True)
