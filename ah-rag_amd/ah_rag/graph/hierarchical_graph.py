@@ -62,6 +62,22 @@ _DEVICE_GRAPHS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
 _SHARED_GRAPHS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
 
 
+def _abspath(path: str) -> str:
+    """os.path.abspath, memoised per (working directory, path): search() resolves the same store path
+    on every call."""
+    cwd = os.getcwd()
+    k = (cwd, path)
+    a = _ABSPATHS.get(k)
+    if a is None:
+        if len(_ABSPATHS) > 1024:
+            _ABSPATHS.clear()
+        a = _ABSPATHS[k] = os.path.abspath(path)
+    return a
+
+
+_ABSPATHS: Dict[Tuple[str, str], str] = {}
+
+
 def _file_stamp(path: str) -> Tuple:
     try:
         st = os.stat(path)
@@ -683,7 +699,7 @@ class HierarchicalGraph:
         """The store at db_path resident in HBM (one copy per store, storage type and GPU in the
         process, shared by every graph object); reloaded whole only when another writer changed the
         file (build_vector_index keeps it current incrementally)."""
-        key = os.path.abspath(db_path)
+        key = _abspath(db_path)
         res = self._indexes.get(key)
         if res is None:
             rkey = self._resident_key(key)
@@ -698,7 +714,7 @@ class HierarchicalGraph:
 
     def search_engine(self, db_path: str) -> SearchEngine:
         graph = self.device_graph()
-        key = os.path.abspath(db_path)
+        key = _abspath(db_path)
         res = self.resident_index(key)
         stamp = (res.version, graph.serial)
         hit = self._engines.get(key)
@@ -752,7 +768,7 @@ class HierarchicalGraph:
         engine = self.search_engine(db_path)
         # Chroma answers n_results > count with every row (:714); only a dense top-k that really
         # needs more than AHR_MAX_K_LARGE rows is out of this index's range
-        if min(top_k, len(engine.index)) > nat.AHR_MAX_K_LARGE:
+        if min(top_k, engine.n_rows) > nat.AHR_MAX_K_LARGE:
             raise ValueError(f"top_k={top_k} exceeds the dense index limit ({nat.AHR_MAX_K_LARGE})")
         if query_vectors is None:
             enc = self._encoder(model_name)
@@ -769,14 +785,6 @@ class HierarchicalGraph:
         return engine, params, rows, scores, res
 
     def _assemble(self, engine: SearchEngine, rows, scores, res, b: int, top_k: int, return_cluster: bool):
-        seeds = []
-        # Chroma's cosine distance of a hit is a float32 (hnswlib: 1 - <q, x> in single precision);
-        # the reference turns it into semantic = 1.0 - float(dist) in double (:719-724)
-        dists = (np.float32(1.0) - np.asarray(scores, np.float32)).tolist()
-        for r, dist in zip(rows.tolist(), dists):
-            if r < 0:
-                continue
-            seeds.append({"node_id": engine.row_ids[r], "semantic": 1.0 - float(dist), "meta": engine.row_metas[r]})
         n_nodes = engine.graph.n_nodes
         nodes = self.G.nodes
         reranked = []
@@ -795,6 +803,14 @@ class HierarchicalGraph:
                              "name": d.get("name"), "title": d.get("title")})
         if not return_cluster:
             return reranked
+        seeds = []
+        # Chroma's cosine distance of a hit is a float32 (hnswlib: 1 - <q, x> in single precision);
+        # the reference turns it into semantic = 1.0 - float(dist) in double (:719-724)
+        dists = (np.float32(1.0) - np.asarray(scores, np.float32)).tolist()
+        for r, dist in zip(rows.tolist(), dists):
+            if r < 0:
+                continue
+            seeds.append({"node_id": engine.row_ids[r], "semantic": 1.0 - float(dist), "meta": engine.row_metas[r]})
         expanded = []
         e = int(res.exp_count[b])
         for idx, src, sem in zip(res.exp_nodes[b, :e].tolist(), res.exp_src[b, :e].tolist(),

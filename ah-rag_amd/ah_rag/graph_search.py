@@ -492,6 +492,7 @@ class SearchEngine:
         rows = np.asarray([graph.index.get(r, n + i) for i, r in enumerate(self.row_ids)], np.int32)
         self.row_to_node_host = rows if len(rows) else np.zeros(1, np.int32)
         self.row_to_node = torch.from_numpy(self.row_to_node_host).to(graph.device)
+        self.n_rows = len(self.row_ids)  # the index's row count when the engine was built (its version)
         self._bufs: Dict[Tuple, Tuple] = {}
         self._hbufs: Dict[Tuple, Tuple] = {}
         # the staging / result buffers are reused across calls: one caller at a time per index
@@ -541,7 +542,7 @@ class SearchEngine:
         result copy and stream wait in one C call, on the current stream (the drop-in search())."""
         B = int(query_vectors.shape[0]) if query_vectors.dim() > 1 else 1
         dim = int(query_vectors.shape[-1])
-        k_dense = min(max(1, params.top_k), max(1, len(self.index)), nat.AHR_MAX_K_LARGE)
+        k_dense = min(max(1, params.top_k), max(1, self.n_rows), nat.AHR_MAX_K_LARGE)
         max_exp = max(1, k_dense * (1 + max(2, params.member_top_m)))
         kk = max(max(params.top_k, 0), 1)
         key = (B, dim, k_dense, max_exp, kk)
@@ -558,18 +559,18 @@ class SearchEngine:
             out = torch.empty(ar_b.value, dtype=torch.uint8, pin_memory=True)
             specs = [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)] + self.graph.rerank_specs(
                 B, k_dense, params)
-            views = _host_views(out.numpy(), specs, list(offs))
-            b = self._hbufs[key] = (ws, ws_b.value, q_host, q_host.numpy(), out, views)
-        ws, ws_bytes, q_host, q_np, out, views = b
+            b = self._hbufs[key] = (ws, ws_b.value, q_host, q_host.numpy(), out, out.numpy(), specs, list(offs))
+        ws, ws_bytes, q_host, q_np, out, out_np, specs, offs = b
         np.copyto(q_np, query_vectors.reshape(B, dim).numpy(), casting="same_kind")
         dev = self.graph.device
         with devtime.span(None, dev):
             nat.check(nat.lib().ahr_search_host(
                 self.index.handle, self.graph._h, q_host.data_ptr(), B, k_dense, self.row_to_node.data_ptr(),
                 int(self.row_to_node.shape[0]), nat.ctypes.byref(params.to_c_cached()), max_exp, ws.data_ptr(),
-                ws_bytes, out.data_ptr(), nat.stream_ptr(torch.cuda.current_stream(dev))), "ahr_search_host")
-        # (copies: the host buffer is the next call's)
-        scores_h, rows_h, *outs = [v.copy() for v in views]
+                ws_bytes, out.data_ptr(), nat.stream_ptr(device_index=dev.index)), "ahr_search_host")
+        # one copy of the whole result buffer (the pinned one is the next call's), views into it
+        host = out_np.copy()
+        scores_h, rows_h, *outs = _host_views(host, specs, offs)
         return rows_h, scores_h, RerankResult(*outs)
 
     def _run(self, query_vectors: torch.Tensor, params: RerankParams,

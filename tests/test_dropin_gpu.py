@@ -178,3 +178,35 @@ def test_incremental_reindex_matches_reference(workdir):
     c = case["post"][0]
     assert isclose_dicts(_norm(hg2.search(c["query"], top_k=8, return_cluster=True, db_path="vector_db_up")),
                          c["result"])
+
+
+def test_concurrent_search_threads(workdir):
+    """Two threads calling search() / search_batch() on one graph at once (the GIL is released
+    during the native calls): the engine's reused staging and result buffers are taken in turns, so
+    every answer equals the serial one (no silent cross-talk)."""
+    import threading
+    d, hg = workdir
+    cases = [c for c in _load("search_cases.json")["cases"] if not c.get("include_hyperedges")][:24]
+    want = [_norm(hg.search(c["query"], return_cluster=c["return_cluster"], **c["params"])) for c in cases]
+    errors = []
+
+    def worker(off):
+        try:
+            for rep in range(6):
+                for i in range(off, len(cases), 2):
+                    c = cases[i]
+                    if rep % 2:
+                        got = hg.search_batch([c["query"], c["query"]], return_cluster=c["return_cluster"],
+                                              **c["params"])[1]
+                    else:
+                        got = hg.search(c["query"], return_cluster=c["return_cluster"], **c["params"])
+                    if _norm(got) != want[i]:
+                        errors.append((off, rep, i))
+        except Exception as e:  # noqa: BLE001 — reported below
+            errors.append(repr(e))
+    ts = [threading.Thread(target=worker, args=(o,)) for o in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:5]

@@ -78,7 +78,7 @@ def main():
                 eng.run(qt, params)
             print(f"SearchEngine.run B = 1: {(time.perf_counter() - t0) / a.envs * 1e3:.4f} ms per call", flush=True)
             (key, b), = [(k, v) for k, v in eng._hbufs.items() if k[0] == 1]
-            ws, ws_bytes, q_host, q_np, out, views = b
+            ws, ws_bytes, q_host, q_np, out = b[:5]
             c = params.to_c_cached()
             args = (eng.index.handle, eng.graph._h, q_host.data_ptr(), 1, key[2], eng.row_to_node.data_ptr(),
                     int(eng.row_to_node.shape[0]), nat.ctypes.byref(c), key[3], ws.data_ptr(), ws_bytes,
