@@ -56,7 +56,8 @@ EXPORTED_SYMBOLS = (
     "ahr_graph_create", "ahr_graph_destroy", "ahr_graph_expand_rerank", "ahr_graph_expand_rerank_rows",
     "ahr_graph_expand", "ahr_graph_expand_ws_bytes", "ahr_graph_expand_host",
     "ahr_graph_lca", "ahr_graph_lca_workspace", "ahr_graph_lca_large", "ahr_graph_info",
-    "ahr_search_layout", "ahr_search_host",
+    "ahr_search_layout", "ahr_search_host", "ahr_graph_env_layout", "ahr_graph_env_step",
+    "ahr_graph_env_step_host",
 )
 
 
@@ -124,6 +125,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ahr_graph_lca_large": ([_P, _P, _I, _I, _I, _P, _P, _P, _L, _P], _I),
         "ahr_graph_info": ([_P, _P, _P], _I),
         "ahr_search_layout": ([_I, _I, _I, _I, _I, _P, _P, _P], _I),
+        "ahr_graph_env_layout": ([_I, _I, _I, _I, _P, _P], _I),
+        "ahr_graph_env_step": ([_P, _I, _I, _I, _I, _I, _P, _L, _P, _L, _P], _I),
+        "ahr_graph_env_step_host": ([_P, _I, _I, _I, _I, _I, _P, _L, _P, _P, _L, _P, _P], _I),
         "ahr_search_host": ([_P, _P, _P, _I, _I, _P, _L, ctypes.POINTER(RerankParams), _I, _P, _L, _P, _P], _I),
     }
     for name, (args, res) in sig.items():

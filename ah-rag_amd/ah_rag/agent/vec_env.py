@@ -7,9 +7,10 @@ VecAHRAGGymEnv keeps N AHRAGGymEnv-equivalent environments over ONE device graph
 their state as arrays rather than N Python environment objects:
   reset(queries)  -> one batched search (dense top-k + expansion + rerank on the GPU, the result
                      arrays taken as they come back, no result dicts built);
-  step(actions)   -> environments that chose the same expansion action share one
-                     ahr_graph_expand launch on the node indices of their selections; commit /
-                     details / end are array updates (plus one small set update per environment);
+  step(actions)   -> one ahr_graph_env_step launch for every environment: expansions, commits,
+                     details and the selection / frontier sets, which live in device memory as
+                     per-environment slot arrays; the state comes back in one copy and is the
+                     step's snapshot (no per-environment Python on the step path);
   observations    -> the 84-d featurizer vectors as one [N, 84] array from per-node feature
                      tables (built once per graph version) and the kernels' outputs.
 The per-environment dicts the gym returns (info["raw_obs"], the search cluster) are built only
@@ -36,7 +37,6 @@ EXPAND_ACTIONS = {0: "parents", 1: "children", 2: "related"}
 K_NODES = 10          # featurizer nodes (featurizer.py:21) = the widest selection (expansion limit 10)
 VEC_DIM = 4 + NODE_FEATS * K_NODES
 OBS_RESET, OBS_EXPAND, OBS_COMMIT, OBS_DETAILS = 0, 1, 2, 3
-_EMPTY = frozenset()
 
 
 class _NodeTable:
@@ -67,9 +67,9 @@ class _NodeTable:
 
 class _ObsBatch:
     """One observation per environment as arrays (what one reset or step produced). Selections
-    hold extended node indices (-1 past sel_n); S / F are the selection / frontier sets at the
-    observation (immutable: the environment replaces, never mutates, a set it changes); alias[e] =
-    (batch, index) where the gym returned the previous observation object itself."""
+    hold extended node indices (-1 past sel_n); the selection / frontier sets the observations show
+    are rows of the state snapshot taken at the step (S_snap / F_snap); alias[e]: the gym returned
+    the previous observation object itself (prev's own e-th one)."""
 
     def __init__(self, E: int) -> None:
         self.kind = np.zeros(E, np.int8)
@@ -81,24 +81,23 @@ class _ObsBatch:
         self.seed_n = np.zeros(E, np.int64)
         self.s_size = np.zeros(E, np.int64)
         self.f_size = np.zeros(E, np.int64)
-        self.S: List[frozenset] = [_EMPTY] * E
-        self.F: List[Any] = [_EMPTY] * E
-        self.alias: Optional[List[Optional[Tuple["_ObsBatch", int]]]] = None
+        # the selection / frontier the observation shows: rows of a state snapshot (the host copy
+        # of the device state after this step; -1 = a removed frontier slot), S row[:s_size], F
+        # row[:f_shown]
+        self.S_snap: Optional[np.ndarray] = None
+        self.F_snap: Optional[np.ndarray] = None
+        self.f_shown = np.zeros(E, np.int64)
+        # alias[e]: environment e's observation is the previous batch's (self.prev) own e-th one
+        self.alias: Optional[np.ndarray] = None
+        self.prev: Optional["_ObsBatch"] = None
         self.cache: Dict[int, Dict[str, Any]] = {}
         self.search = None  # reset: (engine, params, rows, scores, res, seed_idx, seed_sem, seed_n)
         self.stamp = None   # the graph version the observation was taken on (HierarchicalGraph._graph_stamp)
 
-    def copy_rows(self, src: "_ObsBatch", idx: Optional[np.ndarray] = None) -> None:
-        """src's rows idx into this batch (idx None: every row)."""
-        if idx is None:
-            for name in ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size"):
-                getattr(self, name)[:] = getattr(src, name)
-            self.S, self.F = list(src.S), list(src.F)
-            return
-        for name in ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size"):
-            getattr(self, name)[idx] = getattr(src, name)[idx]
-        for e in idx.tolist():
-            self.S[e], self.F[e] = src.S[e], src.F[e]
+    def copy_rows(self, src: "_ObsBatch") -> None:
+        """src's rows into this batch (the defaults of a step: unchanged observations)."""
+        for name in ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size", "f_shown"):
+            getattr(self, name)[:] = getattr(src, name)
 
 
 class LazyInfos(_SequenceABC):
@@ -155,11 +154,11 @@ class _GraphEnvView:
 
     @property
     def selection_set(self) -> set:
-        return {self._v._id(i) for i in self._v._S[self._e]}
+        return {self._v._id(i) for i in self._v._state_rows("S", self._e)}
 
     @property
     def frontier_set(self) -> set:
-        return {self._v._id(i) for i in self._v._F[self._e]}
+        return {self._v._id(i) for i in self._v._state_rows("F", self._e)}
 
 
 class EnvView:
@@ -197,8 +196,13 @@ class VecAHRAGGymEnv:
         self._steps = np.zeros(E, np.int64)         # GraphEnvironment.step_count
         self._cur = np.zeros(E, np.int64)           # AHRAGGymEnv._cur_step
         self._last_action = np.full(E, -1, np.int64)
-        self._S: List[Any] = [_EMPTY] * E           # selection sets (extended node indices)
-        self._F: List[Any] = [_EMPTY] * E           # frontier sets
+        # the environments' selection / frontier sets live in device memory (ahr_graph_env_step:
+        # append-only slot arrays per environment, sized for max_steps steps after a reset and grown
+        # if an environment is stepped further); self._st is the host mirror after the last step
+        self._bufs = None
+        self._st: Optional[np.ndarray] = None
+        self._offs: Optional[List[int]] = None
+        self._fcap = self._scap = 0
         self._obs: Optional[_ObsBatch] = None
         self._reset_batch: Optional[_ObsBatch] = None
         self._queries: Optional[List[str]] = None
@@ -214,10 +218,63 @@ class VecAHRAGGymEnv:
     def _id(self, idx: int) -> str:
         return self._engine.node_id(int(idx))
 
+    # ---- device state ---------------------------------------------------------------------------
+    def _part(self, st: np.ndarray, name: str) -> np.ndarray:
+        """A part of an environment-state buffer (DeviceGraph.ENV_PARTS) as a numpy view."""
+        from ..graph_search import DeviceGraph
+        E, K = self.n_envs, K_NODES
+        i = DeviceGraph.ENV_PARTS.index(name)
+        o = self._offs[i]
+        size = {"sel": E * K, "F": E * self._fcap, "S": E * self._scap, "vec": E * VEC_DIM, "err": 1}.get(name, E)
+        v = st[o:o + size]
+        if name == "vec":
+            return v.view(np.float32).reshape(E, VEC_DIM)
+        return v.reshape(E, -1) if name in ("sel", "F", "S") else v
+
+    def _state_rows(self, which: str, e: int) -> List[int]:
+        """Environment e's current selection (S) or frontier (F) members, extended node indices."""
+        if self._st is None:
+            return []
+        if which == "S":
+            return self._part(self._st, "S")[e, :int(self._part(self._st, "S_n")[e])].tolist()
+        row = self._part(self._st, "F")[e, :int(self._part(self._st, "F_end")[e])]
+        return row[row >= 0].tolist()
+
+    def _alloc_state(self, fcap: int, scap: int) -> None:
+        g = self._engine.graph
+        self._fcap, self._scap = fcap, scap
+        self._bufs, self._st, self._offs = g.env_buffers(self.n_envs, K_NODES, fcap, scap)
+
+    def _grow_state(self) -> None:
+        """Double the frontier / selection capacity, keeping the state (an environment stepped far
+        beyond max_steps without a reset)."""
+        old, ofc, osc = self._st.copy(), self._fcap, self._scap
+        prev_offs = self._offs
+        self._alloc_state(ofc * 2, osc * 2)
+        from ..graph_search import DeviceGraph
+        E, K = self.n_envs, K_NODES
+        for i, name in enumerate(DeviceGraph.ENV_PARTS):
+            o = prev_offs[i]
+            if name == "F":
+                self._part(self._st, "F")[:] = -1
+                self._part(self._st, "F")[:, :ofc] = old[o:o + E * ofc].reshape(E, ofc)
+            elif name == "S":
+                self._part(self._st, "S")[:] = -1
+                self._part(self._st, "S")[:, :osc] = old[o:o + E * osc].reshape(E, osc)
+            elif name == "sel":
+                self._part(self._st, "sel")[:] = old[o:o + E * K].reshape(E, K)
+            elif name == "vec":
+                self._part(self._st, "vec")[:] = old[o:o + E * VEC_DIM].view(np.float32).reshape(E, VEC_DIM)
+            elif name != "err":
+                self._part(self._st, name)[:] = old[o:o + E]
+        self._engine.graph.env_upload(self._bufs, self._st)
+
     def _node_table(self) -> _NodeTable:
         key = (id(self._engine), self.hg._graph_stamp())
         if self._table is None or self._table[0] != key:
-            self._table = (key, _NodeTable(self.hg, self._engine))
+            tab = _NodeTable(self.hg, self._engine)
+            tab.dev = self._engine.graph.env_node_table(tab.feats)  # the step kernel's copy
+            self._table = (key, tab)
         return self._table[1]
 
     def action_masks(self) -> np.ndarray:
@@ -270,9 +327,8 @@ class VecAHRAGGymEnv:
         return [{"node_id": i, "score": a, "semantic": b} for i, a, b in zip(ids, sc, sm)]
 
     def _obs_dict(self, ob: _ObsBatch, e: int) -> Dict[str, Any]:
-        if ob.alias is not None and ob.alias[e] is not None:
-            src, se = ob.alias[e]
-            return self._obs_dict(src, se)
+        while ob.alias is not None and ob.alias[e]:
+            ob = ob.prev
         d = ob.cache.get(e)
         if d is not None:
             return d
@@ -282,8 +338,9 @@ class VecAHRAGGymEnv:
         if kind == OBS_DETAILS:
             d = g._bare_observation([g._details(self._id(ob.sel[e, 0]))] if n else [], step=step)
         else:
-            S = {self._id(i) for i in ob.S[e]}
-            F = {self._id(i) for i in ob.F[e]}
+            S = {self._id(i) for i in ob.S_snap[e, :int(ob.s_size[e])].tolist()}
+            fr = ob.F_snap[e, :int(ob.f_shown[e])]
+            F = {self._id(i) for i in fr[fr >= 0].tolist()}
             if kind == OBS_RESET:
                 _, _, _, _, _, seed_idx, seed_sem, seed_n = ob.search
                 seeds = self._briefs(seed_idx[e], int(seed_n[e]), None, seed_sem[e])
@@ -347,16 +404,31 @@ class VecAHRAGGymEnv:
         ob.seed_n[:] = seed_n
         ob.search = (engine, params, rows, scores, res, seed_idx, seed_sem, seed_n)
         ob.stamp = self.hg._graph_stamp()
-        # selection cleared; frontier = the reranked nodes
-        self._S = [_EMPTY] * E
-        self._F = [frozenset(r[:c]) for r, c in zip(ob.sel.tolist(), n_out.tolist())]
-        ob.S = list(self._S)
-        ob.F = list(self._F)
-        ob.f_size[:] = [len(f) for f in self._F]
+        # selection cleared; frontier = the reranked nodes (distinct): the device state of the batch
+        fcap = K_NODES * (self.max_steps + 2)
+        scap = 3 * (self.max_steps + 2)
+        if self._bufs is None or self._fcap < fcap or self._scap < scap or self._bufs[0].device != engine.graph.device:
+            self._alloc_state(max(fcap, 32), max(scap, 8))
+        st = self._st
+        self._part(st, "sel")[:] = ob.sel
+        self._part(st, "sel_n")[:] = ob.sel_n
+        F = self._part(st, "F")
+        F[:] = -1
+        F[:, :K_NODES] = ob.sel
+        self._part(st, "F_end")[:] = n_out
+        self._part(st, "F_n")[:] = n_out
+        self._part(st, "S")[:] = -1
+        self._part(st, "S_n")[:] = 0
+        ob.S_snap, ob.F_snap = self._part(st, "S").copy(), F.copy()
+        ob.f_shown[:] = n_out
+        ob.f_size[:] = n_out
         self._cur[:] = 0
         self._last_action[:] = -1
         self._obs = self._reset_batch = ob
         vecs = self._featurize(ob)
+        self._part(st, "step")[:] = 1
+        self._part(st, "vec")[:] = vecs  # an unchanged observation keeps its vector on the device
+        engine.graph.env_upload(self._bufs, st)
 
         def info(e: int) -> Dict[str, Any]:
             d: Dict[str, Any] = {"raw_obs": self._obs_dict(ob, e), "aux": self._aux(ob, e)}
@@ -374,86 +446,46 @@ class VecAHRAGGymEnv:
         if a.shape != (E,):
             raise ValueError("one action per environment")
         self._cur += 1
-        n_graph = self._engine.graph.n_nodes
         ob = _ObsBatch(E)
         ob.copy_rows(prev)  # the defaults: unchanged (aliased) observations
-        ob.alias = [None] * E
         ob.search = prev.search
         ob.stamp = self.hg._graph_stamp()
-        pos = np.arange(K_NODES)[None, :]
-        top_valid = pos < prev.sel_n[:, None]
 
-        # expansions (environment.py:393-480): one ahr_graph_expand launch per action kind, all
-        # enqueued before one host copy (one stream sync per step, not one per kind)
-        launched = []
-        for act, name in EXPAND_ACTIONS.items():
-            g = np.flatnonzero(a == act)
-            if not len(g):
-                continue
-            t = TOP_IDS[act]
-            inp = np.where(top_valid[g, :t] & (prev.sel[g, :t] < n_graph), prev.sel[g, :t], -1)
-            launched.append((g, *self._engine.graph.expand(name, torch.from_numpy(inp.astype(np.int32)), K_NODES)))
-        host = to_host_arrays(*[x for _, out, cnt in launched for x in (out, cnt)])
-        for i, (g, _, _) in enumerate(launched):
-            out_h, cnt_h = host[2 * i].astype(np.int64), host[2 * i + 1].astype(np.int64)
-            self._steps[g] += 1
-            ob.kind[g] = OBS_EXPAND
-            ob.step[g] = self._steps[g]
-            ob.sel[g] = np.where(pos < cnt_h[:, None], out_h[:, :K_NODES], -1)
-            ob.sel_n[g] = cnt_h
-            ob.score[g] = 0.0
-            ob.sem[g] = 0.0
-            ob.seed_n[g] = cnt_h
-            # the observation shows the frontier before this expansion's ids join it (:292-300)
-            for e, row, c in zip(g.tolist(), out_h.tolist(), cnt_h.tolist()):
-                F = self._F[e]
-                ob.S[e], ob.F[e] = self._S[e], F
-                ob.s_size[e], ob.f_size[e] = len(self._S[e]), len(F)
-                if c:
-                    self._F[e] = F.union(row[:c])
-
-        # commit_selection of the top 3 (environment.py:327-341)
-        for e in np.flatnonzero(a == 3).tolist():
-            S, F = self._S[e], self._F[e]
-            added = []
-            for x in prev.sel[e, :min(3, int(prev.sel_n[e]))].tolist():
-                if x < n_graph and x not in S:
-                    if not added:
-                        S, F = set(S), set(F)
-                    S.add(x)
-                    added.append(x)
-                    F.discard(x)
-            self._S[e], self._F[e] = S, F
-            self._steps[e] += 1
-            ob.kind[e] = OBS_COMMIT
-            ob.step[e] = self._steps[e]
-            ob.sel[e] = -1
-            ob.sel[e, :len(added)] = added
-            ob.sel_n[e] = len(added)
-            ob.score[e] = 0.0
-            ob.sem[e] = 0.0
-            ob.seed_n[e] = 0
-            ob.S[e], ob.F[e] = S, F
-            ob.s_size[e], ob.f_size[e] = len(S), len(F)
-
-        # query_node_details of the top 1 (environment.py:301-325); none: the previous observation
-        det = np.flatnonzero((a == 4) & (prev.sel_n > 0))
-        if len(det):
-            node = prev.sel[det, 0]
-            in_g = node < n_graph
-            self._steps[det] += 1
-            ob.kind[det] = OBS_DETAILS
-            ob.step[det] = self._steps[det]
-            ob.sel[det] = -1
-            ob.sel[det, 0] = np.where(in_g, node, -1)
-            ob.sel_n[det] = in_g.astype(np.int64)
-            ob.score[det] = 0.0
-            ob.sem[det] = 0.0
-            ob.seed_n[det] = 0
-        # end_episode, and any action past the five (gym_env.py _apply's last branch): done, same observation
+        # the step on the device (ahr_graph_env_step, one C call): expansions of the top 2 / 2 / 1
+        # (environment.py:393-480), commits of the top 3 (:340-355), details of the top 1
+        # (:301-335), the frontier / selection sets updated in device memory; the whole state comes
+        # back as this step's snapshot (the observation dicts are built from it on demand)
+        graph = self._engine.graph
+        st = self._st
+        if int(self._part(st, "F_end").max(initial=0)) + K_NODES > self._fcap or \
+                int(self._part(st, "S_n").max(initial=0)) + 3 > self._scap:
+            self._grow_state()
+            st = self._st
+        self._part(st, "actions")[:] = a
+        tab = self._node_table()
+        graph.env_step(self._bufs, st, E, K_NODES, self._fcap, self._scap, K_NODES, tab.dev)
+        if self._part(st, "err")[0]:
+            raise RuntimeError("environment state capacity exceeded (ahr_graph_env_step)")
+        snap = st.copy()
+        kind = self._part(snap, "kind")
+        moved = kind > 0
+        self._steps[:] = self._part(snap, "step")
+        ob.step[moved] = self._steps[moved]
+        ob.kind[moved] = np.where(kind[moved] == 1, OBS_EXPAND, np.where(kind[moved] == 2, OBS_COMMIT, OBS_DETAILS))
+        ob.sel[moved] = self._part(snap, "sel")[moved]
+        ob.sel_n[moved] = self._part(snap, "sel_n")[moved]
+        ob.score[moved] = 0.0
+        ob.sem[moved] = 0.0
+        ob.seed_n[moved] = self._part(snap, "seed_n")[moved]
+        sf = moved & (kind != 3)  # expansions and commits show the sets
+        ob.s_size[sf] = self._part(snap, "s_size")[sf]
+        ob.f_size[sf] = self._part(snap, "f_size")[sf]
+        ob.f_shown[sf] = self._part(snap, "f_shown")[sf]
+        ob.S_snap, ob.F_snap = self._part(snap, "S"), self._part(snap, "F")
+        # end_episode, and any action past the five (gym_env.py _apply's last branch), and details of
+        # an empty selection: the same observation
         ends = (a < 0) | (a > 4)
-        for e in np.flatnonzero(((a == 4) & (prev.sel_n == 0)) | ends).tolist():
-            ob.alias[e] = prev.alias[e] if prev.alias is not None and prev.alias[e] is not None else (prev, e)
+        ob.alias, ob.prev = ~moved, prev
 
         # rewards (reward.py:6-26 on the raw observations; a details observation has no "state")
         pf, cf = prev.kind != OBS_DETAILS, ob.kind != OBS_DETAILS
@@ -468,7 +500,14 @@ class VecAHRAGGymEnv:
         done = done | (self._cur >= self.max_steps)
         self._last_action = a
         self._obs = ob
-        vecs = self._featurize(ob)
+        # the observations' vectors, written by the step kernel from the node table (an unchanged
+        # observation keeps its own); environments showing a node whose attributes the featurizer
+        # cannot convert take the reference's path (featurize_observation on the dict: it raises)
+        vecs = self._part(snap, "vec")
+        valid = np.arange(K_NODES)[None, :] < ob.sel_n[:, None]
+        bad = moved & (tab.bad[np.where(valid, ob.sel, 0)] & valid).any(axis=1)
+        for e in np.flatnonzero(bad).tolist():
+            vecs[e] = featurize_observation(self._obs_dict(ob, e), K_NODES)[0]
         cur = self._cur.copy()
 
         def info(e: int) -> Dict[str, Any]:

@@ -299,6 +299,52 @@ class DeviceGraph:
                 nat.stream_ptr(torch.cuda.current_stream(self.device))), "ahr_graph_expand_host")
         return res_np[:B * lim].reshape(B, lim).copy(), res_np[B * lim:].copy()
 
+    # -- vectorised environment state (VecAHRAGGymEnv) -----------------------------------------
+    ENV_PARTS = ("actions", "sel", "sel_n", "F", "F_end", "F_n", "S", "S_n", "kind", "seed_n", "f_shown", "f_size",
+                 "s_size", "step", "vec", "err")
+
+    @staticmethod
+    def env_layout(E: int, K: int, fcap: int, scap: int) -> Tuple[List[int], int]:
+        """(int32 element offsets of ahr_graph_env_layout's parts, total bytes)."""
+        offs = (nat.ctypes.c_int64 * 16)()
+        nbytes = nat.ctypes.c_int64()
+        nat.check(nat.lib().ahr_graph_env_layout(E, K, fcap, scap, offs, nat.ctypes.byref(nbytes)),
+                  "ahr_graph_env_layout")
+        return list(offs), nbytes.value
+
+    def env_buffers(self, E: int, K: int, fcap: int, scap: int):
+        """(device workspace, pinned host mirror as an int32 numpy array, element offsets) of one
+        environment batch's state (ahr_graph_env_step)."""
+        offs, nbytes = self.env_layout(E, K, fcap, scap)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        host = torch.zeros(nbytes // 4, dtype=torch.int32, pin_memory=True)
+        return (ws, host), host.numpy(), offs
+
+    def env_node_table(self, feats: np.ndarray) -> torch.Tensor:
+        """The featurizer's node table [m][6] (float64 on the host) as the fp32 device table
+        ahr_graph_env_step reads (each value rounded once, as featurize_observation does)."""
+        return torch.from_numpy(np.ascontiguousarray(feats, np.float32)).to(self.device)
+
+    def env_upload(self, bufs, host_np: np.ndarray) -> None:
+        """The host mirror's state -> the device workspace (after a reset)."""
+        ws, host = bufs
+        with torch.cuda.device(self.device):
+            ws.view(torch.int32).copy_(host, non_blocking=True)
+
+    def env_step(self, bufs, host_np: np.ndarray, E: int, K: int, fcap: int, scap: int, limit: int,
+                 feats: Optional[torch.Tensor] = None) -> None:
+        """One step of the environments whose actions sit in host_np's actions part: the kernel
+        updates the device state (and, given the device node table `feats` [m][6] fp32, writes the
+        new observations' featurizer vectors), and the whole workspace comes back into host_np (one
+        C call)."""
+        ws, host = bufs
+        with devtime.span(None, self.device):
+            nat.check(nat.lib().ahr_graph_env_step_host(
+                self._h, E, K, fcap, scap, limit, nat.ptr(feats), 0 if feats is None else int(feats.shape[0]),
+                host.data_ptr(), ws.data_ptr(), ws.numel(), host.data_ptr(),
+                nat.stream_ptr(device_index=self.device.index)), "ahr_graph_env_step_host")
+
+
 @dataclass
 class RerankParams:
     alpha: float

@@ -355,17 +355,11 @@ struct Emit {
 // (every membership test then an L2 round trip).
 constexpr int kExpLds = 32;
 
-template <bool kLds>
-__global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
-                                                    const int32_t* __restrict__ inputs, int B,
-                                                    int n_in, int limit, int32_t* __restrict__ out,
-                                                    int32_t* __restrict__ out_count) {
-  __shared__ int32_t sbuf[kLds ? kExpLds * 64 : 1];
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= B) return;
-  Emit em{kLds ? sbuf + threadIdx.x : out + (int64_t)q * limit, kLds ? 64 : 1, limit, 0, 0};
+// One environment's expansion (environment.py:393-480) of the node indices inputs[0 .. n_in) into em.
+__device__ __forceinline__ void expand_one(const DevGraph& g, int action, const int32_t* inputs, int n_in, int limit,
+                                           Emit& em) {
   for (int i = 0; i < n_in && !em.full(); ++i) {
-    const int32_t nid = inputs[(int64_t)q * n_in + i];
+    const int32_t nid = inputs[i];
     if (nid < 0 || nid >= g.n_nodes) continue;  // `if nid not in self.hg.G: continue`
     if (action == 0 || action == 1) {
       // 0: successors with belongs_to (expand_parents :424-426)
@@ -391,9 +385,160 @@ __global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
     }
     if (em.raw >= limit) break;  // `if len(expanded) >= limit: break`
   }
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(64) void expand_kernel(DevGraph g, int action,
+                                                    const int32_t* __restrict__ inputs, int B,
+                                                    int n_in, int limit, int32_t* __restrict__ out,
+                                                    int32_t* __restrict__ out_count) {
+  __shared__ int32_t sbuf[kLds ? kExpLds * 64 : 1];
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  Emit em{kLds ? sbuf + threadIdx.x : out + (int64_t)q * limit, kLds ? 64 : 1, limit, 0, 0};
+  expand_one(g, action, inputs + (int64_t)q * n_in, n_in, limit, em);
   if constexpr (kLds)
     for (int i = 0; i < em.n; ++i) out[(int64_t)q * limit + i] = sbuf[i * 64 + threadIdx.x];
   out_count[q] = em.n;
+}
+
+// One step of E environments of VecAHRAGGymEnv (gym_env.py:77-125 over environment.py:301-355,
+// :393-480), their state resident in device memory (one thread per environment):
+//   actions 0-2  expansion of the current selection's top 2 / 2 / 1 graph nodes (limit K): the
+//                observation shows the selection = the expansion and the frontier BEFORE its ids
+//                join it (f_shown = the frontier slots it shows); then frontier |= expansion;
+//   action 3     commit of the top 3: graph nodes not yet selected join the selection (appended)
+//                and leave the frontier (their slot set to -1); the observation shows the added ids;
+//   action 4     details of the top node (a selection of it alone if it is a graph node; none if
+//                the selection is empty: then, like any other action, the previous observation);
+//   else         end / invalid: the observation is the previous one (kind -1), no state change.
+// State: sel [E][K] / sel_n (the current observation's selection, rewritten in place), frontier F
+// [E][fcap] (append-only slots, -1 = removed) / F_end (slots used) / F_n (members), selection S
+// [E][scap] / S_n. A full frontier or selection sets *err (the host grows the buffers first).
+// With a node table (feats [n_feat][6]: is_entity, is_summary, is_other, layer, judge, confidence
+// per extended node index) each new observation's featurizer vector is written too (vec [E][4 + 8 K],
+// step [E] the environments' step counters).
+constexpr int kEnvTop[5] = {2, 2, 1, 3, 1};
+
+__global__ __launch_bounds__(64) void env_step_kernel(DevGraph g, int E, int K, int fcap, int scap, int limit,
+                                                      const int32_t* __restrict__ actions, int32_t* __restrict__ sel,
+                                                      int32_t* __restrict__ sel_n, int32_t* __restrict__ F,
+                                                      int32_t* __restrict__ F_end, int32_t* __restrict__ F_n,
+                                                      int32_t* __restrict__ S, int32_t* __restrict__ S_n,
+                                                      int32_t* __restrict__ kind, int32_t* __restrict__ seed_n,
+                                                      int32_t* __restrict__ f_shown, int32_t* __restrict__ f_size,
+                                                      int32_t* __restrict__ s_size, int32_t* __restrict__ step,
+                                                      float* __restrict__ vec, int32_t* __restrict__ err,
+                                                      const float* __restrict__ feats, int64_t n_feat) {
+  __shared__ int32_t sbuf[kExpLds * 64];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int a = actions[e];
+  const int n = sel_n[e];
+  int32_t* my_sel = sel + (int64_t)e * K;
+  int32_t top[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int32_t x = j < n && j < K ? my_sel[j] : -1;
+    top[j] = x >= 0 && x < g.n_nodes ? x : -1;  // graph nodes only (`if nid in self.hg.G`)
+  }
+  int32_t* myF = F + (int64_t)e * fcap;
+  int32_t* myS = S + (int64_t)e * scap;
+  int fe = F_end[e], fn = F_n[e], sn = S_n[e];
+  int k_out = -1;
+  int f_obs = 0;  // the frontier size the new observation shows (before an expansion's union)
+  if (a >= 0 && a <= 2) {
+    Emit em{sbuf + threadIdx.x, 64, limit, 0, 0};
+    expand_one(g, a, top, kEnvTop[a], limit, em);
+    f_shown[e] = fe;
+    f_size[e] = fn;
+    f_obs = fn;
+    s_size[e] = sn;
+    for (int i = 0; i < K; ++i) my_sel[i] = i < em.n ? sbuf[i * 64 + threadIdx.x] : -1;
+    sel_n[e] = em.n;
+    seed_n[e] = em.n;
+    for (int i = 0; i < em.n; ++i) {  // frontier |= expansion
+      const int32_t v = sbuf[i * 64 + threadIdx.x];
+      bool found = false;
+      for (int j = 0; j < fe && !found; ++j) found = myF[j] == v;
+      if (found) continue;
+      if (fe >= fcap) {
+        *err = 1;
+        break;
+      }
+      myF[fe++] = v;
+      ++fn;
+    }
+    k_out = 1;
+  } else if (a == 3) {
+    int32_t added[3];
+    int na = 0;
+    for (int j = 0; j < 3 && j < n; ++j) {
+      const int32_t x = top[j];
+      if (x < 0) continue;
+      bool in_s = false;
+      for (int i = 0; i < sn && !in_s; ++i) in_s = myS[i] == x;
+      if (in_s) continue;
+      if (sn >= scap) {
+        *err = 1;
+        break;
+      }
+      myS[sn++] = x;
+      added[na++] = x;
+      for (int i = 0; i < fe; ++i)
+        if (myF[i] == x) {  // `self.frontier_set.discard(nid)`
+          myF[i] = -1;
+          --fn;
+          break;
+        }
+    }
+    for (int i = 0; i < K; ++i) my_sel[i] = i < na ? added[i] : -1;
+    sel_n[e] = na;
+    seed_n[e] = 0;
+    f_shown[e] = fe;
+    f_size[e] = fn;
+    s_size[e] = sn;
+    f_obs = fn;
+    k_out = 2;
+  } else if (a == 4 && n > 0) {
+    const int32_t node = n > 0 && K > 0 ? my_sel[0] : -1;
+    const bool in_g = node >= 0 && node < g.n_nodes;
+    for (int i = 0; i < K; ++i) my_sel[i] = i == 0 && in_g ? node : -1;
+    sel_n[e] = in_g ? 1 : 0;
+    seed_n[e] = 0;
+    k_out = 3;
+  }
+  F_end[e] = fe;
+  F_n[e] = fn;
+  S_n[e] = sn;
+  kind[e] = k_out;
+  if (k_out < 0 || !feats) return;  // the previous observation: its vector stays
+  // the observation's 4 + 8 K featurizer vector (featurizer.py:21-56): [step, |selection|,
+  // min(|frontier|, 50), |seeds|] + per shown node [is_entity, is_summary, is_other, layer, score,
+  // semantic, judge_overall, confidence] from the node table (score and semantic are 0 after a
+  // step); a details observation has no state (zeros)
+  const int stp = step[e] + 1;
+  step[e] = stp;
+  float* v = vec + (int64_t)e * (4 + 8 * K);
+  const bool full = k_out != 3;
+  v[0] = (float)stp;
+  v[1] = full ? (float)sn : 0.f;
+  v[2] = full ? (float)(f_obs < 50 ? f_obs : 50) : 0.f;
+  v[3] = (float)seed_n[e];
+  const int ns = sel_n[e];
+  for (int i = 0; i < K; ++i) {
+    float* b = v + 4 + 8 * i;
+    const int32_t x = i < ns ? my_sel[i] : -1;
+    const float* f = x >= 0 && x < n_feat ? feats + (int64_t)x * 6 : nullptr;
+    b[0] = f ? f[0] : 0.f;
+    b[1] = f ? f[1] : 0.f;
+    b[2] = f ? f[2] : 0.f;
+    b[3] = f ? f[3] : 0.f;
+    b[4] = 0.f;
+    b[5] = 0.f;
+    b[6] = f ? f[4] : 0.f;
+    b[7] = f ? f[5] : 0.f;
+  }
 }
 
 // launch on B queries (one thread each)
@@ -849,6 +994,57 @@ int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int
 static int64_t expand_ws_bytes(int B, int n_in, int limit) {
   auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
   return al((int64_t)B * n_in * 4) + al((int64_t)B * (limit > 0 ? limit : 1) * 4) + al((int64_t)B * 4);
+}
+
+int ahr_graph_env_layout(int E, int K, int fcap, int scap, int64_t offsets[16], int64_t* bytes) {
+  if (!offsets || !bytes) return fail(AHR_EINVAL, "null output");
+  if (E < 1 || K < 1 || fcap < 1 || scap < 1) return fail(AHR_EINVAL, "sizes must be >= 1");
+  const int64_t e = E;
+  const int64_t part[16] = {e, e * K, e, e * fcap, e, e, e * scap, e, e, e, e, e, e, e, e * (4 + 8 * K), 1};
+  int64_t o = 0;
+  for (int i = 0; i < 16; ++i) {
+    offsets[i] = o;
+    o += (part[i] + 63) / 64 * 64;  // int32 elements, 256-B aligned parts
+  }
+  *bytes = o * 4;
+  return AHR_OK;
+}
+
+int ahr_graph_env_step(ahr_graph* g, int E, int K, int fcap, int scap, int limit, const float* node_feats,
+                       int64_t n_feat, void* ws, int64_t ws_bytes, void* stream) {
+  if (!g || !ws) return fail(AHR_EINVAL, "null graph or workspace");
+  if (limit < 0 || limit > kExpLds || K < 3 || K < limit) return fail(AHR_EINVAL, "need 3 <= K, limit <= K, limit <= 32");
+  if (n_feat < 0) return fail(AHR_EINVAL, "negative node table size");
+  int64_t off[16], need = 0;
+  const int st = ahr_graph_env_layout(E, K, fcap, scap, off, &need);
+  if (st != AHR_OK) return st;
+  if (ws_bytes < need) return fail(AHR_EINVAL, "workspace smaller than ahr_graph_env_layout's bytes");
+  int32_t* w = static_cast<int32_t*>(ws);
+  DeviceGuardG dg(g->device);
+  hipLaunchKernelGGL(env_step_kernel, dim3((E + 63) / 64), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), g->dg, E,
+                     K, fcap, scap, limit, w + off[0], w + off[1], w + off[2], w + off[3], w + off[4], w + off[5],
+                     w + off[6], w + off[7], w + off[8], w + off[9], w + off[10], w + off[11], w + off[12], w + off[13],
+                     reinterpret_cast<float*>(w + off[14]), w + off[15], node_feats, n_feat);
+  AHR_HIP(hipGetLastError());
+  return AHR_OK;
+}
+
+int ahr_graph_env_step_host(ahr_graph* g, int E, int K, int fcap, int scap, int limit, const float* node_feats,
+                            int64_t n_feat, const int32_t* host_actions, void* ws, int64_t ws_bytes, int32_t* host_out,
+                            void* stream) {
+  if (!host_actions || !host_out) return fail(AHR_EINVAL, "null host buffer");
+  int64_t off[16], need = 0;
+  int st = ahr_graph_env_layout(E, K, fcap, scap, off, &need);
+  if (st != AHR_OK) return st;
+  if (!ws || ws_bytes < need) return fail(AHR_EINVAL, "workspace smaller than ahr_graph_env_layout's bytes");
+  DeviceGuardG dg(g ? g->device : 0);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  AHR_HIP(hipMemcpyAsync(ws, host_actions, (size_t)E * 4, hipMemcpyHostToDevice, s));
+  st = ahr_graph_env_step(g, E, K, fcap, scap, limit, node_feats, n_feat, ws, ws_bytes, stream);
+  if (st != AHR_OK) return st;
+  AHR_HIP(hipMemcpyAsync(host_out, ws, (size_t)need, hipMemcpyDeviceToHost, s));
+  AHR_HIP(hipStreamSynchronize(s));
+  return AHR_OK;
 }
 
 int ahr_graph_expand_ws_bytes(int B, int n_in, int limit, int64_t* bytes) {

@@ -304,6 +304,33 @@ int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, 
                           int limit, int32_t* host_out, int32_t* host_count, void* ws, int64_t ws_bytes,
                           void* stream);
 
+/* One step of E vectorised RL environments with their state in device memory (VecAHRAGGymEnv;
+ * gym_env.py:77-125 over environment.py:301-355 commit / details and :393-480 expansions): per
+ * environment, action 0-2 expands the current selection's top 2 / 2 / 1 graph nodes (limit
+ * `limit`; the observation shows the expansion and the frontier before its ids join it), 3 commits
+ * the top 3 (graph nodes not yet selected join the selection and leave the frontier), 4 shows the
+ * top node's details, anything else (end, invalid, details of an empty selection) keeps the
+ * previous observation. The workspace ws (int32, ahr_graph_env_layout's 16 parts, each 256-B
+ * aligned; host-only arithmetic) holds, in order: actions [E] (in), the selection sel [E][K] and
+ * sel_n [E] (in: the current observation's, out: the new one's), frontier F [E][fcap] (-1 =
+ * removed), F_end [E] (slots used), F_n [E], selection set S [E][scap], S_n [E], then the
+ * observation outputs kind [E] (1 expansion, 2 commit, 3 details, -1 the previous observation),
+ * seed_n [E], f_shown [E] (the frontier slots the observation shows), f_size [E], s_size [E], the
+ * environments' step counters step [E], the observations' featurizer vectors vec [E][4 + 8 K] (fp32
+ * bits, featurizer.py:21-56; written for a new observation when node_feats is given: fp32 [n_feat][6]
+ * = is_entity, is_summary, is_other, layer, judge_overall, confidence per extended node index),
+ * and err [1] (set to 1 when a frontier or selection would overflow its capacity: grow and retry
+ * from saved state). Needs 3 <= K, limit <= K and limit <= 32. Enqueued on `stream`. */
+int ahr_graph_env_layout(int E, int K, int fcap, int scap, int64_t offsets[16], int64_t* bytes);
+int ahr_graph_env_step(ahr_graph* g, int E, int K, int fcap, int scap, int limit, const float* node_feats,
+                       int64_t n_feat, void* ws, int64_t ws_bytes, void* stream);
+/* The same from the host in one call: host_actions [E] int32 are copied into the workspace, the step
+ * runs, the whole workspace (state and observation outputs) is copied back into host_out (int32,
+ * the layout's bytes) and the stream is waited for. Host buffers should be pinned. */
+int ahr_graph_env_step_host(ahr_graph* g, int E, int K, int fcap, int scap, int limit, const float* node_feats,
+                            int64_t n_feat, const int32_t* host_actions, void* ws, int64_t ws_bytes, int32_t* host_out,
+                            void* stream);
+
 /* Batched GraphEnvironment.expand_to_lca (environment.py:243-299): per query the nodes of the
  * intersection of the inputs' "ancestors or self" sets on the belongs_to DAG (nx.ancestors: nodes
  * with a belongs_to path to the input) that have no belongs_to out-edge to another member.

@@ -37,6 +37,85 @@ class _HostGraph:
         self.index = {n: i for i, n in enumerate(self.ids)}
         self.n_nodes = len(self.ids)
 
+    # ahr_graph_env_step restated on the host over the oracle's expansions (environment.py:301-355,
+    # :393-480 on the environments' slot arrays; include/ahr.h documents the kernel's contract)
+    def env_buffers(self, E, K, fcap, scap):
+        from ah_rag.graph_search import DeviceGraph
+        offs, nbytes = DeviceGraph.env_layout(E, K, fcap, scap)
+        return None, np.zeros(nbytes // 4, np.int32), offs
+
+    def env_upload(self, bufs, host):
+        pass
+
+    def env_node_table(self, feats):
+        return np.asarray(feats, np.float32)
+
+    def env_step(self, bufs, st, E, K, fcap, scap, limit, feats=None):
+        from ah_rag.graph_search import DeviceGraph
+        offs, _ = DeviceGraph.env_layout(E, K, fcap, scap)
+        part = {n: st[offs[i]:] for i, n in enumerate(DeviceGraph.ENV_PARTS)}
+        sel, F, S = part["sel"][:E * K].reshape(E, K), part["F"][:E * fcap].reshape(E, fcap), \
+            part["S"][:E * scap].reshape(E, scap)
+        n_g = self.n_nodes
+        for e in range(E):
+            a, n = int(part["actions"][e]), int(part["sel_n"][e])
+            top = [int(x) if 0 <= x < n_g else -1 for x in sel[e, :min(n, 3)]]
+            fe, fn, sn = int(part["F_end"][e]), int(part["F_n"][e]), int(part["S_n"][e])
+            kind = -1
+            if 0 <= a <= 2:
+                names = [self.ids[x] for x in top[:(2, 2, 1)[a]] if x >= 0]
+                out = [self.index[i] for i in search_ref.env_expand(self.G, ("parents", "children", "related")[a],
+                                                                     names, limit)]
+                part["f_shown"][e], part["f_size"][e], part["s_size"][e] = fe, fn, sn
+                sel[e] = -1
+                sel[e, :len(out)] = out
+                part["sel_n"][e] = part["seed_n"][e] = len(out)
+                for v in out:
+                    if v not in F[e, :fe].tolist():
+                        F[e, fe] = v
+                        fe += 1
+                        fn += 1
+                kind = 1
+            elif a == 3:
+                added = []
+                for x in top[:3]:
+                    if x >= 0 and x not in S[e, :sn].tolist():
+                        S[e, sn] = x
+                        sn += 1
+                        added.append(x)
+                        hit = np.flatnonzero(F[e, :fe] == x)
+                        if len(hit):
+                            F[e, hit[0]] = -1
+                            fn -= 1
+                sel[e] = -1
+                sel[e, :len(added)] = added
+                part["sel_n"][e], part["seed_n"][e] = len(added), 0
+                part["f_shown"][e], part["f_size"][e], part["s_size"][e] = fe, fn, sn
+                kind = 2
+            elif a == 4 and n > 0:
+                node = int(sel[e, 0])
+                sel[e] = -1
+                if node < n_g:
+                    sel[e, 0] = node
+                part["sel_n"][e], part["seed_n"][e] = int(node < n_g), 0
+                kind = 3
+            part["F_end"][e], part["F_n"][e], part["S_n"][e], part["kind"][e] = fe, fn, sn, kind
+            if kind > 0 and feats is not None:  # the featurizer vector of the new observation
+                part["step"][e] += 1
+                vec = part["vec"][:E * (4 + 8 * K)].view(np.float32).reshape(E, 4 + 8 * K)
+                full = kind != 3
+                ns = int(part["sel_n"][e])
+                f_obs = int(part["f_size"][e])
+                row = [float(part["step"][e]), float(sn) if full else 0.0, float(min(f_obs, 50)) if full else 0.0,
+                       float(part["seed_n"][e])]
+                for i in range(K):
+                    if i < ns:
+                        f = feats[int(sel[e, i])]
+                        row += [f[0], f[1], f[2], f[3], 0.0, 0.0, f[4], f[5]]
+                    else:
+                        row += [0.0] * 8
+                vec[e] = np.asarray(row, np.float32)
+
     def expand(self, action, inputs, limit=10, stream=None):
         x = inputs.numpy()
         out = np.full((x.shape[0], limit), -1, np.int32)
