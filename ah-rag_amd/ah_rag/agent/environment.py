@@ -72,6 +72,8 @@ class GraphEnvironment:
                 pass
         self._count_cache: Optional[Tuple[Tuple, Dict[str, int]]] = None
         self._dag_cache: Optional[Tuple[Tuple, bool, Set[str]]] = None
+        self._brief_cache: Dict[str, Dict[str, Any]] = {}
+        self._brief_stamp: Optional[Tuple] = None
         self._ensure_graph_loaded()
 
     # ---- plumbing ----------------------------------------------------------------------------
@@ -106,12 +108,22 @@ class GraphEnvironment:
         return dict(self._count_cache[1])
 
     def _node_brief(self, node_id: str) -> Dict[str, Any]:
-        d = self.hg.G.nodes.get(node_id, {})
-        kind = d.get("node_type")
-        return {"node_id": node_id, "node_type": kind, "entity_type": d.get("entity_type"),
-                "layer": 0 if kind == "entity" else (d.get("level") or (1 if kind == "summary" else 0)),
-                "title": d.get("title"), "name": d.get("name"),
-                "judge_overall": parse_judge(d.get("judge_scores")), "confidence": d.get("confidence")}
+        """The node's brief (reference :104-116) as a fresh dict. The static part is built once per
+        node and graph version (the same stamp that invalidates the device graph: attribute edits
+        go through the graph's mutators, which bump it)."""
+        stamp = self.hg._graph_stamp()
+        if self._brief_stamp != stamp:
+            self._brief_cache, self._brief_stamp = {}, stamp
+        b = self._brief_cache.get(node_id)
+        if b is None:
+            d = self.hg.G.nodes.get(node_id, {})
+            kind = d.get("node_type")
+            b = {"node_id": node_id, "node_type": kind, "entity_type": d.get("entity_type"),
+                 "layer": 0 if kind == "entity" else (d.get("level") or (1 if kind == "summary" else 0)),
+                 "title": d.get("title"), "name": d.get("name"),
+                 "judge_overall": parse_judge(d.get("judge_scores")), "confidence": d.get("confidence")}
+            self._brief_cache[node_id] = b
+        return dict(b)
 
     def _brief_scored(self, res: Dict[str, Any]) -> Dict[str, Any]:
         b = self._node_brief(res.get("node_id"))

@@ -88,6 +88,8 @@ class DeviceGraph:
 
     def __init__(self, G: nx.DiGraph, device: Optional[torch.device] = None) -> None:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
+        _d = torch.device(self.device)
+        self._dev_index = _d.index if _d.index is not None else torch.cuda.current_device()
         self._xbufs: Dict[Tuple[int, int, int], Tuple] = {}  # expand_host's buffers per shape
         self._xlock = threading.Lock()  # expand_host: one caller at a time on the reused buffers
         self.serial = next(_GRAPH_SERIALS)
@@ -288,15 +290,23 @@ class DeviceGraph:
             ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=self.device)
             x_host = torch.empty((B, n_in), dtype=torch.int32, pin_memory=True)
             res = torch.empty(B * lim + B, dtype=torch.int32, pin_memory=True)  # out [B][lim], then count [B]
-            b = (ws, ws_bytes, x_host, x_host.numpy(), res, res.numpy())
+            # (tensors kept alive by the tuple; their addresses resolved once)
+            b = (ws, x_host, res, x_host.numpy(), res.numpy(),
+                 (nat.ptr(x_host), B, n_in, int(limit), nat.ptr(res), nat.ptr(res) + 4 * B * lim, nat.ptr(ws),
+                  ws_bytes))
             self._xbufs[key] = b
-        ws, ws_bytes, x_host, x_np, res, res_np = b
+        x_np, res_np, args = b[3], b[4], b[5]
         np.copyto(x_np, idx, casting="same_kind")
-        with devtime.span(None, self.device):
-            nat.check(nat.lib().ahr_graph_expand_host(
-                self._h, ACTIONS[action], nat.ptr(x_host), B, n_in, int(limit), nat.ptr(res),
-                nat.ptr(res) + 4 * B * lim, nat.ptr(ws), ws_bytes,
-                nat.stream_ptr(torch.cuda.current_stream(self.device))), "ahr_graph_expand_host")
+        # (small batches: the library passes the inputs as kernel arguments and the kernel stores the
+        # results straight into the pinned buffer, ahr_graph_expand_host)
+        if devtime._pairs is None:
+            st = nat.lib().ahr_graph_expand_host(self._h, ACTIONS[action], *args,
+                                                 nat.stream_ptr(None, self._dev_index))
+        else:
+            with devtime.span(None, self.device):
+                st = nat.lib().ahr_graph_expand_host(self._h, ACTIONS[action], *args,
+                                                     nat.stream_ptr(None, self._dev_index))
+        nat.check(st, "ahr_graph_expand_host")
         return res_np[:B * lim].reshape(B, lim).copy(), res_np[B * lim:].copy()
 
     # -- vectorised environment state (VecAHRAGGymEnv) -----------------------------------------

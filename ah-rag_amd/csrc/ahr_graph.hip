@@ -541,6 +541,34 @@ __global__ __launch_bounds__(64) void env_step_kernel(DevGraph g, int E, int K, 
   }
 }
 
+// The single environment's expansion straight from and to the host: the inputs travel in the
+// kernel arguments and the results are stored into pinned host memory, so the call is one launch
+// and one stream wait (no copy operations, each a few microseconds of latency at this size).
+constexpr int kSmallIn = 16;
+struct SmallInputs {
+  int32_t v[kSmallIn];
+};
+
+__global__ __launch_bounds__(64) void expand_small_kernel(DevGraph g, int action, SmallInputs in, int B, int n_in,
+                                                          int limit, int32_t* __restrict__ out,
+                                                          int32_t* __restrict__ out_count) {
+  __shared__ int32_t sbuf[kExpLds * 64];
+  const int q = threadIdx.x;
+  if (q >= B) return;
+  int32_t x[kSmallIn];
+#pragma unroll
+  for (int i = 0; i < kSmallIn; ++i) x[i] = in.v[i];
+  int32_t mine[kSmallIn];
+  int m = 0;
+#pragma unroll
+  for (int i = 0; i < kSmallIn; ++i)
+    if (i >= q * n_in && i < (q + 1) * n_in) mine[m++] = x[i];
+  Emit em{sbuf + threadIdx.x, 64, limit, 0, 0};
+  expand_one(g, action, mine, n_in, limit, em);
+  for (int i = 0; i < em.n; ++i) out[(int64_t)q * (limit > 0 ? limit : 1) + i] = sbuf[i * 64 + threadIdx.x];
+  out_count[q] = em.n;
+}
+
 // launch on B queries (one thread each)
 inline void launch_expand(hipStream_t s, const DevGraph& dg, int action, const int32_t* inputs, int B, int n_in,
                           int limit, int32_t* out, int32_t* out_count) {
@@ -1065,6 +1093,22 @@ int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, 
   DeviceGuardG dg(g->device);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int lim = limit > 0 ? limit : 1;
+  // small batches into pinned host buffers: one launch, no copies (the outputs' device addresses:
+  // pinned host memory is mapped; pageable memory takes the copy path below)
+  if ((int64_t)B * n_in <= kSmallIn && B <= 64 && limit <= kExpLds) {
+    void *d_out = nullptr, *d_cnt = nullptr;
+    if (hipHostGetDevicePointer(&d_out, host_out, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&d_cnt, host_count, 0) == hipSuccess) {
+      SmallInputs in{};
+      for (int i = 0; i < B * n_in; ++i) in.v[i] = host_inputs[i];
+      hipLaunchKernelGGL(expand_small_kernel, dim3(1), dim3(64), 0, s, g->dg, action, in, B, n_in, limit,
+                         static_cast<int32_t*>(d_out), static_cast<int32_t*>(d_cnt));
+      AHR_HIP(hipGetLastError());
+      AHR_HIP(hipStreamSynchronize(s));
+      return AHR_OK;
+    }
+    (void)hipGetLastError();  // (pageable memory: clear the lookup's error, copy path)
+  }
   auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
   int32_t* d_in = static_cast<int32_t*>(ws);
   int32_t* d_out = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + al((int64_t)B * n_in * 4));

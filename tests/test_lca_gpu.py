@@ -91,7 +91,9 @@ def test_lca_over_capacity_matches_oracle(cuda):
 def test_expand_host_matches_device_expand(cuda):
     """ahr_graph_expand_host (host in, host out, one call; reused per-shape buffers) returns what
     ahr_graph_expand writes on the device, for every action, ragged inputs (-1 padding), limits 0,
-    1 and 10, and batch shapes met more than once (the buffers are reused)."""
+    1, 10 and 32, batch shapes met more than once (the buffers are reused), the small-batch path
+    (B * n_in <= 16: inputs as kernel arguments, results stored into the pinned buffer) and the
+    copy path, and pageable host buffers (which always take the copy path)."""
     import torch
     from ah_rag.graph.hierarchical_graph import HierarchicalGraph
     hg = HierarchicalGraph.load(os.path.join(GOLDEN, "reference_graph"))
@@ -100,7 +102,8 @@ def test_expand_host_matches_device_expand(cuda):
     rng = np.random.default_rng(11)
     for rep in range(2):
         for action in ("parents", "children", "related"):
-            for B, n_in, limit in ((1, 3, 10), (1, 1, 1), (7, 5, 10), (64, 2, 0), (33, 4, 3)):
+            for B, n_in, limit in ((1, 3, 10), (1, 1, 1), (7, 5, 10), (64, 2, 0), (33, 4, 3), (4, 4, 10),
+                                     (16, 1, 32), (2, 8, 5), (1, 0, 3), (3, 5, 0)):
                 idx = np.full((B, n_in), -1, np.int32)
                 for b in range(B):
                     m = int(rng.integers(0, n_in + 1))
@@ -112,3 +115,18 @@ def test_expand_host_matches_device_expand(cuda):
                 assert np.array_equal(cnt_h, cnt_d), (action, B, n_in, limit)
                 for b in range(B):
                     assert np.array_equal(out_h[b, :cnt_h[b]], out_d[b, :cnt_d[b]]), (action, B, b)
+                # the same call through pageable numpy buffers (direct C call)
+                from ah_rag import _native as nat
+                lim = max(limit, 1)
+                res = np.zeros(B * lim + B, np.int32)
+                x = np.ascontiguousarray(idx)
+                need = nat.ctypes.c_int64()
+                nat.check(nat.lib().ahr_graph_expand_ws_bytes(B, n_in, limit, nat.ctypes.byref(need)), "ws")
+                ws = torch.empty(max(need.value, 8), dtype=torch.uint8, device=dg.device)
+                nat.check(nat.lib().ahr_graph_expand_host(
+                    dg._h, {"parents": 0, "children": 1, "related": 2}[action], x.ctypes.data, B, n_in, limit,
+                    res.ctypes.data, res.ctypes.data + 4 * B * lim, ws.data_ptr(), need.value,
+                    nat.stream_ptr(None, dg._dev_index)), "ahr_graph_expand_host")
+                assert np.array_equal(res[B * lim:], cnt_d), (action, B, n_in, limit)
+                for b in range(B):
+                    assert np.array_equal(res[b * lim:b * lim + cnt_d[b]], out_d[b, :cnt_d[b]]), (action, B, b)

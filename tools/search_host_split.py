@@ -1,0 +1,57 @@
+"""Host-time split of the drop-in search() at B = 1 (diagnostic): the C5 graph and fp32 store of
+tools/bench_env.py, then per call the pieces of HierarchicalGraph.search_batch timed on their own
+(argument resolution, engine lookup, the native call, the result dicts) over N calls each.
+usage: python tools/search_host_split.py [--n 2000]"""
+import argparse
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ah-rag_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ah_rag.graph_search import resolve_search_params  # noqa: E402
+from ah_rag.synthetic import HOTPOT_90K, SyntheticCorpus, build_hotpot_graph, install_vectors  # noqa: E402
+
+
+def per_call(fn, n):
+    fn()
+    t = time.perf_counter()
+    for _ in range(n):
+        fn()
+    return round((time.perf_counter() - t) / n * 1e6, 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=2000)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    corpus = SyntheticCorpus(HOTPOT_90K, dev)
+    vectors = corpus.rows().cpu().numpy()
+    hg, ids = build_hotpot_graph(corpus, np.random.default_rng(20251003))
+    install_vectors(hg, ids, vectors, os.path.join(tempfile.mkdtemp(prefix="ahr_split_"), "vector_db"))
+    q, _ = corpus.queries(4, corpus.rows())
+    qv = q.cpu().numpy()[:1]
+    qt = torch.from_numpy(qv.copy())
+    sp = hg.G.graph.get("search_params", {})
+    db = hg.G.graph["vector_index"]["db_path"]
+    eng, params, rows, scores, res = hg.search_arrays(["q"], top_k=5, member_top_m=5, query_vectors=qv)
+    out = {
+        "search_batch": per_call(lambda: hg.search_batch(["q"], top_k=5, member_top_m=5, query_vectors=qv), a.n),
+        "search_arrays": per_call(lambda: hg.search_arrays(["q"], top_k=5, member_top_m=5, query_vectors=qv), a.n),
+        "resolve_search_params": per_call(lambda: resolve_search_params(sp, 5, 5, *([None] * 7)), a.n),
+        "search_engine": per_call(lambda: hg.search_engine(db), a.n),
+        "engine.run": per_call(lambda: eng.run(qt, params), a.n),
+        "_assemble": per_call(lambda: hg._assemble(eng, rows[0], scores[0], res, 0, 5, False), a.n),
+        "_assemble(return_cluster)": per_call(lambda: hg._assemble(eng, rows[0], scores[0], res, 0, 5, True), a.n),
+    }
+    print(out, flush=True)
+
+
+if __name__ == "__main__":
+    main()
