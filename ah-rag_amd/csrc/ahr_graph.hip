@@ -1095,7 +1095,12 @@ int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, 
   const int lim = limit > 0 ? limit : 1;
   // small batches into pinned host buffers: one launch, no copies (the outputs' device addresses:
   // pinned host memory is mapped; pageable memory takes the copy path below)
-  if ((int64_t)B * n_in <= kSmallIn && B <= 64 && limit <= kExpLds) {
+  // AHR_EXPAND_SMALL=0 (A/B): every batch takes the copy path
+  static const bool small_on = [] {
+    const char* e = getenv("AHR_EXPAND_SMALL");
+    return !e || atoi(e) != 0;
+  }();
+  if (small_on && (int64_t)B * n_in <= kSmallIn && B <= 64 && limit <= kExpLds) {
     void *d_out = nullptr, *d_cnt = nullptr;
     if (hipHostGetDevicePointer(&d_out, host_out, 0) == hipSuccess &&
         hipHostGetDevicePointer(&d_cnt, host_count, 0) == hipSuccess) {

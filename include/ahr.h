@@ -298,7 +298,9 @@ int ahr_graph_expand(ahr_graph* g, int action, const int32_t* inputs, int B, int
  * workspace, expands, copies out [B][max(limit, 1)] and out_count [B] back into host_out /
  * host_count and waits for the stream. ws: device memory of at least the *bytes that
  * ahr_graph_expand_ws_bytes(B, n_in, limit, &bytes) returns (host-only arithmetic). Host buffers should be pinned (hipHostMalloc / torch pin_memory) for
- * asynchronous copies; pageable ones work, slower. */
+ * asynchronous copies; pageable ones work, slower. Small batches (B * n_in <= 16, limit <= 32)
+ * with pinned outputs take one launch and no copies: the inputs travel as kernel arguments and the
+ * kernel stores the results into the pinned buffers (the single environment's expansion). */
 int ahr_graph_expand_ws_bytes(int B, int n_in, int limit, int64_t* bytes);
 int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, int B, int n_in,
                           int limit, int32_t* host_out, int32_t* host_count, void* ws, int64_t ws_bytes,

@@ -7,7 +7,9 @@ the vector store (no encoder weights offline), then times
   * vec:    VecAHRAGGymEnv with E environments: one batched reset (dense top-5 + expansion +
             rerank for all E queries) and `steps` batched steps of random valid actions;
   * single: the drop-in AHRAGGymEnv stepped one environment at a time (B = 1 per call), the
-            reference's own loop shape (policy_ppo.py:145,163-214) on the device graph.
+            reference's own loop shape (policy_ppo.py:145,163-214) on the device graph: one
+            untimed pass over its episodes, then the median of three timed passes (each reported:
+            a pass is ~20 ms, so one host stall moves a single pass by tens of percent).
 Replicas per GPU: --gpus N runs one process per GPU (spawned by this script, or
 under torch.distributed.run), the graph and corpus replicated, the --envs environments
 partitioned over the ranks; no collective on the data path (the job time is the slowest rank's).
@@ -199,13 +201,20 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
             for a in (0, 1, 2, 3, 4, 0):
                 env.step(a if env.get_action_mask()[a] else random_actions(rng, [env.get_action_mask()])[0])
         torch.cuda.synchronize()
-        ts = time.perf_counter()
-        for i in range(n1):
-            # reset with a precomputed vector (the search at B = 1)
-            single_reset(env, hg, queries[i], qv[i:i + 1])
-            for _ in range(steps):
-                env.step(random_actions(rng, [env.get_action_mask()])[0])
-        single_rate = round(n1 * (1 + steps) / (time.perf_counter() - ts), 1)
+
+        def single_pass():
+            ts = time.perf_counter()
+            for i in range(n1):
+                # reset with a precomputed vector (the search at B = 1)
+                single_reset(env, hg, queries[i], qv[i:i + 1])
+                for _ in range(steps):
+                    env.step(random_actions(rng, [env.get_action_mask()])[0])
+            return n1 * (1 + steps) / (time.perf_counter() - ts)
+        # one untimed pass over the same episodes (first visits: the node briefs, the per-shape
+        # buffers), then three timed passes; the median is the rate, all three are reported
+        single_pass()
+        single_passes = [round(single_pass(), 1) for _ in range(3)]
+        single_rate = float(np.median(single_passes))
         # the drop-in search itself: HierarchicalGraph.search's body at B = 1 (dense top-5 + expansion
         # + rerank + the result dicts, return_cluster=False) with a precomputed query vector
         n_s = min(256, envs)
@@ -238,6 +247,7 @@ def measure(dev, envs: int, steps: int, single: int = 64, rank: int = 0, world: 
             "how": "device = HIP-event spans around every search / expansion pass (ah_rag.devtime) on the "
                    "launch stream, summed; host = wall - device; means over the timed episodes"},
         "single_env_steps_per_s": single_rate,
+        "single_env_passes": single_passes if rank == 0 and single > 0 else None,
         "dropin_search_b1": None if search_s is None else {
             "calls_per_s": round(1.0 / search_s, 1), "ms_per_call": round(search_s * 1e3, 4),
             "what": "HierarchicalGraph.search_batch([q], top_k=5, return_cluster=False) wall time per "

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--envs", type=int, default=64)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--search", action="store_true")
+    ap.add_argument("--reps", type=int, default=1, help="timed loops (each rate printed)")
+    ap.add_argument("--no-brief-cache", action="store_true",
+                    help="A/B: build every node brief from the graph (the round-5 form)")
     ap.add_argument("--raw", action="store_true",
                     help="with --search: also time SearchEngine.run and the bare ahr_search_host call (the floor)")
     a = ap.parse_args()
@@ -44,6 +47,17 @@ def main():
     qv = q.cpu().numpy()
     env = AHRAGGymEnv(max_steps=a.steps + 1, graph=hg)
     env.env.logging_enabled = False
+    if a.no_brief_cache:
+        from ah_rag.graph_search import parse_judge
+
+        def brief(node_id):
+            d = hg.G.nodes.get(node_id, {})
+            kind = d.get("node_type")
+            return {"node_id": node_id, "node_type": kind, "entity_type": d.get("entity_type"),
+                    "layer": 0 if kind == "entity" else (d.get("level") or (1 if kind == "summary" else 0)),
+                    "title": d.get("title"), "name": d.get("name"),
+                    "judge_overall": parse_judge(d.get("judge_scores")), "confidence": d.get("confidence")}
+        env.env._node_brief = brief
 
     def episode(i):
         if a.search:
@@ -55,10 +69,13 @@ def main():
 
     episode(a.envs)  # warm-up
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.envs):
-        episode(i)
-    wall = time.perf_counter() - t0
+    for rep in range(a.reps):
+        t0 = time.perf_counter()
+        for i in range(a.envs):
+            episode(i)
+        wall = time.perf_counter() - t0
+        if a.reps > 1 and not a.search:
+            print(f"rep {rep}: {a.envs * (1 + a.steps) / wall:.1f} env-steps/s", flush=True)
     prof = cProfile.Profile()
     prof.enable()
     for i in range(a.envs):
