@@ -107,14 +107,21 @@ class GraphEnvironment:
                                          "n_edges": self.hg.G.number_of_edges()})
         return dict(self._count_cache[1])
 
-    def _node_brief(self, node_id: str) -> Dict[str, Any]:
-        """The node's brief (reference :104-116) as a fresh dict. The static part is built once per
-        node and graph version (the same stamp that invalidates the device graph: attribute edits
-        go through the graph's mutators, which bump it)."""
+    def _briefs(self) -> Dict[str, Dict[str, Any]]:
+        """The node-brief cache of the current graph version (emptied when the graph's stamp — the
+        one that invalidates the device graph — changes; attribute edits go through the graph's
+        mutators, which bump it)."""
         stamp = self.hg._graph_stamp()
         if self._brief_stamp != stamp:
             self._brief_cache, self._brief_stamp = {}, stamp
-        b = self._brief_cache.get(node_id)
+        return self._brief_cache
+
+    def _node_brief(self, node_id: str, cache: Optional[Dict[str, Dict[str, Any]]] = None) -> Dict[str, Any]:
+        """The node's brief (reference :104-116) as a fresh dict; its static part built once per node
+        and graph version (`cache`: the caller's _briefs(), fetched once per observation)."""
+        if cache is None:
+            cache = self._briefs()
+        b = cache.get(node_id)
         if b is None:
             d = self.hg.G.nodes.get(node_id, {})
             kind = d.get("node_type")
@@ -122,11 +129,11 @@ class GraphEnvironment:
                  "layer": 0 if kind == "entity" else (d.get("level") or (1 if kind == "summary" else 0)),
                  "title": d.get("title"), "name": d.get("name"),
                  "judge_overall": parse_judge(d.get("judge_scores")), "confidence": d.get("confidence")}
-            self._brief_cache[node_id] = b
+            cache[node_id] = b
         return dict(b)
 
-    def _brief_scored(self, res: Dict[str, Any]) -> Dict[str, Any]:
-        b = self._node_brief(res.get("node_id"))
+    def _brief_scored(self, res: Dict[str, Any], cache: Optional[Dict[str, Dict[str, Any]]] = None) -> Dict[str, Any]:
+        b = self._node_brief(res.get("node_id"), cache)
         b["score"] = res.get("score")
         b["semantic"] = res.get("semantic")
         return b
@@ -138,9 +145,10 @@ class GraphEnvironment:
                         frontier_set, step: int) -> Dict[str, Any]:
         """The observation dict (reference :118-150) for the given state; VecAHRAGGymEnv builds its
         environments' observations through this from their state snapshots."""
+        cache = self._briefs()
         obs: Dict[str, Any] = {
-            "selection": [self._brief_scored(x) for x in reranked],
-            "seeds": [self._brief_scored(x) for x in seeds],
+            "selection": [self._brief_scored(x, cache) for x in reranked],
+            "seeds": [self._brief_scored(x, cache) for x in seeds],
             "state": {"selection_ids": sorted(selection_set),
                       "frontier_ids": sorted(frontier_set)[:50]},
             "counts": self._counts(),
@@ -384,9 +392,15 @@ def expand_batch(hg: HierarchicalGraph, action: str, inputs: Sequence[Sequence[s
     """One ahr_graph_expand launch for many environments: inputs[b] are env b's node ids."""
     dg = hg.device_graph()
     width = max(1, max((len(x) for x in inputs), default=1))
-    idx = np.full((len(inputs), width), -1, np.int32)
-    for b, ids in enumerate(inputs):
-        if ids:
-            idx[b, :len(ids)] = dg.node_indices(ids)
+    if len(inputs) == 1:  # the single environment's call: one row, no per-row numpy writes
+        get = dg.index.get
+        row = [get(x, -1) for x in inputs[0]]
+        idx = np.array([row + [-1] * (width - len(row))], np.int32)
+    else:
+        idx = np.full((len(inputs), width), -1, np.int32)
+        for b, ids in enumerate(inputs):
+            if ids:
+                idx[b, :len(ids)] = dg.node_indices(ids)
     out_h, cnt_h = dg.expand_host(action, idx, limit)
-    return [[dg.ids[i] for i in out_h[b, :cnt_h[b]]] for b in range(len(inputs))]
+    names = dg.ids
+    return [[names[i] for i in out_h[b, :cnt_h[b]].tolist()] for b in range(len(inputs))]

@@ -27,11 +27,17 @@ def node_row(n: Dict[str, Any]) -> List[float]:
 def featurize_observation(obs: Dict[str, Any], k_nodes: int = 10) -> Tuple[np.ndarray, Dict[str, Any]]:
     state = obs.get("state") or {}
     sel = (obs.get("selection") or [])[:k_nodes]
-    # one Python list, one float32 conversion (each value rounded once from double, as before)
+    # one Python list, one float32 conversion (each value rounded once from double, as before);
+    # node_row inlined (the single environment featurizes every step)
     row = [_num(obs.get("step")), float(len(state.get("selection_ids") or [])),
            float(len(state.get("frontier_ids") or [])), float(len(obs.get("seeds") or []))]
     for n in sel:
-        row.extend(node_row(n))
+        g = n.get
+        kind = str(g("node_type") or "")
+        ent, summ = kind == "entity", kind == "summary"
+        row += (float(ent), float(summ), float(not (ent or summ)), float(g("layer") or 0.0),
+                float(g("score") or 0.0), float(g("semantic") or 0.0), float(g("judge_overall") or 0.0),
+                float(g("confidence") or 0.0))
     row.extend([0.0] * (NODE_FEATS * (k_nodes - len(sel))))
     vec = np.array(row, np.float32)
     return vec, {"top_node_ids": [str(n.get("node_id")) for n in sel]}
