@@ -55,6 +55,12 @@ namespace qres {
 // a 3-slot ring issued two blocks ahead), 48-KiB stages a 2-slot ring issued one stage ahead.
 constexpr int kLandBytes = 768;
 
+// Issue priority (A/B build switch): 0 none; 1 static s_setprio 1 for waves 4-7 (the younger half,
+// the VALU-arbitration loser) before the main loop; 2 s_setprio 1 around every block's MFMA chain.
+#ifndef AHR_QRES_PRIO
+#define AHR_QRES_PRIO 0
+#endif
+
 static_assert(kPark >= 6, "the replay of a parked block never overtakes its unread quads");
 
 #ifndef AHR_QRES_PB6
@@ -94,8 +100,11 @@ static_assert(Cfg<12>::kLds <= 160 * 1024 && Cfg<6>::kLds <= 160 * 1024,
 // From block 32 on (large corpora) the schedule continues every 8 blocks to block 127, then every
 // 128: a publication after block 8m - 2 (128m - 2) and an event at the end of block 8m - 1.
 constexpr uint32_t kSeedWaitTicks = 1000;  // s_memrealtime ticks (100 MHz): a 10-us bound per wait
+#ifndef AHR_QRES_LATE
+#define AHR_QRES_LATE 128  // the event period from block 128 on (A/B build switch, a power of two)
+#endif
 __device__ __forceinline__ bool in_sched(uint32_t mask, int bi, int off) {
-  return bi < 32 ? ((mask >> bi) & 1) != 0 : (bi + off) % (bi < 128 ? 8 : 128) == 0;
+  return bi < 32 ? ((mask >> bi) & 1) != 0 : (bi + off) % (bi < 128 ? 8 : AHR_QRES_LATE) == 0;
 }
 
 // k-th largest of the wave's nonzero values (lane l holds v0, v1); 0 if fewer than k are nonzero.
@@ -617,6 +626,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
   // v_permlane16_swap per register pair gives each lane the 32x32 form's share — one query (lane %
   // 32) and 16 rows — so the screening below is the same code (quad rows: quad_row).
   auto stage_mma = [&](int st, int h = 0) __attribute__((always_inline)) {
+    if constexpr (AHR_QRES_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (C::kMma16) {
       f32x4 c[4];
 #pragma unroll
@@ -660,6 +670,7 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    if constexpr (AHR_QRES_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   };
   auto finish_block = [&](int bi) __attribute__((always_inline)) {  // bi: the block just multiplied
     if constexpr (skip_screen) {  // GEMM only: the chain kept live (rule 17), no top-k
@@ -680,6 +691,9 @@ __global__ __launch_bounds__(kThreads, 2) void topk_qres_kernel(
     screen_quads(acc, r0);
     if (ss && in_sched((uint32_t)sched, bi, 2)) publish();
   };
+  if constexpr (AHR_QRES_PRIO == 1) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // wave: readfirstlane, so a scalar branch
+  }
   stamp(2);
   {  // iteration 0, peeled: the sync waits only for stage 0's pieces (the fragments are younger)
     if (!(ABL & ABL_NOWAIT)) {  // younger than stage 0's pieces: the other prologue stages', the fragments

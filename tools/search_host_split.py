@@ -50,6 +50,26 @@ def main():
         "_assemble": per_call(lambda: hg._assemble(eng, rows[0], scores[0], res, 0, 5, False), a.n),
         "_assemble(return_cluster)": per_call(lambda: hg._assemble(eng, rows[0], scores[0], res, 0, 5, True), a.n),
     }
+    # the pieces of SearchEngine._run_host (graph_search.py) on their own
+    from ah_rag import _native as nat
+    from ah_rag.graph_search import _host_views
+    eng.run(qt, params)
+    b = next(iter(eng._hbufs.values()))
+    ws, ws_bytes, q_host, q_np, ob, out_np, specs, offs = b
+    k_dense = specs[0][0][1]
+    max_exp = specs[2][0][1]
+    stream = nat.stream_ptr(device_index=dev.index)
+    cp = params.to_c_cached()
+    lib = nat.lib()
+
+    def bare():
+        lib.ahr_search_host(eng.index.handle, eng.graph._h, q_host.data_ptr(), 1, k_dense, eng.row_to_node.data_ptr(),
+                            int(eng.row_to_node.shape[0]), nat.ctypes.byref(cp), max_exp, ws.data_ptr(), ws_bytes,
+                            ob.data_ptr(), stream)
+
+    out["native_call"] = per_call(bare, a.n)
+    out["copy+views"] = per_call(lambda: _host_views(out_np.copy(), specs, offs), a.n)
+    out["stream_ptr"] = per_call(lambda: nat.stream_ptr(device_index=dev.index), a.n)
     print(out, flush=True)
 
 
