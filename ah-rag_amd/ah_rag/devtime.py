@@ -28,6 +28,11 @@ def recording():
         _pairs = prev
 
 
+def active() -> bool:
+    """Whether spans are being recorded (callers on a hot path skip span() when not)."""
+    return _pairs is not None
+
+
 @contextlib.contextmanager
 def span(stream: Optional[torch.cuda.Stream] = None, device: Optional[torch.device] = None):
     """A HIP event pair around the launches issued inside the block (on `stream`, or the

@@ -745,11 +745,12 @@ class HierarchicalGraph:
                      return_cluster: bool = False, db_path: Optional[str] = None,
                      model_name: Optional[str] = None, query_vectors: Optional[np.ndarray] = None) -> List[Any]:
         """search() over many queries with one device pass (B = len(queries))."""
-        engine, params, rows, scores, res = self.search_arrays(
-            queries, top_k, member_top_m, alpha, beta, gamma, delta, judge_overall_min, confidence_min, type_filter,
-            db_path, model_name, query_vectors)
-        return [self._assemble(engine, rows[b], scores[b], res, b, params.top_k, return_cluster)
-                for b in range(rows.shape[0])]
+        def assemble(engine, params, rows, scores, res):
+            return [self._assemble(engine, rows[b], scores[b], res, b, params.top_k, return_cluster)
+                    for b in range(rows.shape[0])]
+
+        return self._search_arrays(queries, top_k, member_top_m, alpha, beta, gamma, delta, judge_overall_min,
+                                   confidence_min, type_filter, db_path, model_name, query_vectors, assemble)
 
     def search_arrays(self, queries: Sequence[str], top_k: int = 5, member_top_m: int = 5,
                       alpha: Optional[float] = None, beta: Optional[float] = None, gamma: Optional[float] = None,
@@ -760,6 +761,14 @@ class HierarchicalGraph:
         """search_batch() before the result dicts: (engine, params, dense rows [B,k], dense scores
         [B,k], host RerankResult); _assemble(engine, rows[b], scores[b], res, b, ...) turns query b
         into search()'s return value. VecAHRAGGymEnv works on these arrays directly."""
+        return self._search_arrays(queries, top_k, member_top_m, alpha, beta, gamma, delta, judge_overall_min,
+                                   confidence_min, type_filter, db_path, model_name, query_vectors, None)
+
+    def _search_arrays(self, queries, top_k, member_top_m, alpha, beta, gamma, delta, judge_overall_min,
+                       confidence_min, type_filter, db_path, model_name, query_vectors, consume):
+        """search_arrays(); with `consume`, its result goes to consume(engine, params, rows, scores,
+        res) under the engine's lock instead, as views of the engine's result buffer (no copy: a
+        small host batch's arrays are overwritten by the next call), and its return value is returned."""
         params = resolve_search_params(self.G.graph.get("search_params", {}), top_k, member_top_m, alpha, beta,
                                        gamma, delta, judge_overall_min, confidence_min, type_filter)
         vi = self.G.graph.get("vector_index") if isinstance(self.G.graph.get("vector_index"), dict) else {}
@@ -777,12 +786,18 @@ class HierarchicalGraph:
             query_vectors = enc.encode(list(queries), normalize_embeddings=True, **extra)
         if isinstance(query_vectors, torch.Tensor):
             q = query_vectors.to(torch.float32)
-        else:
-            q = torch.from_numpy(np.ascontiguousarray(np.asarray(query_vectors, np.float32)))
-        if q.dim() == 1:
-            q = q.unsqueeze(0)
-        rows, scores, res = engine.run(q, params)
-        return engine, params, rows, scores, res
+            if q.dim() == 1:
+                q = q.unsqueeze(0)
+        else:  # host vectors go to the engine as numpy (its one-call path stages them itself)
+            q = np.asarray(query_vectors, np.float32)
+            if q.ndim == 1:
+                q = q.reshape(1, -1)
+        if consume is None:
+            rows, scores, res = engine.run(q, params)
+            return engine, params, rows, scores, res
+        with engine._lock:
+            rows, scores, res = engine.run(q, params, borrow=True)
+            return consume(engine, params, rows, scores, res)
 
     def _assemble(self, engine: SearchEngine, rows, scores, res, b: int, top_k: int, return_cluster: bool):
         n_nodes = engine.graph.n_nodes

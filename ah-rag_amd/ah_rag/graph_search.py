@@ -583,20 +583,28 @@ class SearchEngine:
 
     HOST_PATH_MAX_B = 64  # host query batches up to this size take ahr_search_host (one C call)
 
-    def run(self, query_vectors: torch.Tensor, params: RerankParams,
-            stream: Optional[torch.cuda.Stream] = None) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
-        """Dense top_k -> expansion -> rerank for a batch. Returns host (rows, scores, result)."""
+    def run(self, query_vectors, params: RerankParams, stream: Optional[torch.cuda.Stream] = None,
+            borrow: bool = False) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
+        """Dense top_k -> expansion -> rerank for a batch (a torch tensor, or a host numpy array).
+        Returns host (rows, scores, result). borrow=True (the caller holds self._lock until it has
+        read them): a small host batch's arrays are views of the engine's pinned result buffer,
+        which the next call overwrites — no copy (search_batch assembles its dicts under the lock)."""
         with self._lock:
+            if isinstance(query_vectors, np.ndarray):
+                B = int(query_vectors.shape[0]) if query_vectors.ndim > 1 else 1
+                if stream is None and 1 <= B <= self.HOST_PATH_MAX_B:
+                    return self._run_host(query_vectors, params, borrow)
+                query_vectors = torch.from_numpy(np.ascontiguousarray(query_vectors, np.float32))
             if stream is None and query_vectors.device.type == "cpu" and \
                     1 <= (query_vectors.shape[0] if query_vectors.dim() > 1 else 1) <= self.HOST_PATH_MAX_B:
-                return self._run_host(query_vectors, params)
+                return self._run_host(query_vectors.numpy(), params, borrow)
             return self._run(query_vectors, params, stream)
 
-    def _run_host(self, query_vectors: torch.Tensor, params: RerankParams
+    def _run_host(self, query_vectors: np.ndarray, params: RerankParams, borrow: bool = False
                   ) -> Tuple[np.ndarray, np.ndarray, RerankResult]:
         """A small host batch through ahr_search_host: query copy, dense top-k, expansion + rerank,
         result copy and stream wait in one C call, on the current stream (the drop-in search())."""
-        B = int(query_vectors.shape[0]) if query_vectors.dim() > 1 else 1
+        B = int(query_vectors.shape[0]) if query_vectors.ndim > 1 else 1
         dim = int(query_vectors.shape[-1])
         k_dense = min(max(1, params.top_k), max(1, self.n_rows), nat.AHR_MAX_K_LARGE)
         max_exp = max(1, k_dense * (1 + max(2, params.member_top_m)))
@@ -615,18 +623,28 @@ class SearchEngine:
             out = torch.empty(ar_b.value, dtype=torch.uint8, pin_memory=True)
             specs = [((B, k_dense), torch.float32), ((B, k_dense), torch.int32)] + self.graph.rerank_specs(
                 B, k_dense, params)
-            b = self._hbufs[key] = (ws, ws_b.value, q_host, q_host.numpy(), out, out.numpy(), specs, list(offs))
-        ws, ws_bytes, q_host, q_np, out, out_np, specs, offs = b
-        np.copyto(q_np, query_vectors.reshape(B, dim).numpy(), casting="same_kind")
+            out_np = out.numpy()
+            scores_b, rows_b, *outs_b = _host_views(out_np, specs, list(offs))
+            # (the fixed arguments of the C call, resolved once per buffer set)
+            fixed = (self.graph._h, q_host.data_ptr(), B, k_dense, self.row_to_node.data_ptr(),
+                     int(self.row_to_node.shape[0]))
+            b = self._hbufs[key] = (ws, ws_b.value, q_host.numpy(), out, out_np, specs, list(offs), fixed,
+                                    (rows_b, scores_b, RerankResult(*outs_b)), q_host)
+        ws, ws_bytes, q_np, out, out_np, specs, offs, fixed, borrowed, _ = b
+        np.copyto(q_np, query_vectors.reshape(B, dim), casting="same_kind")
         dev = self.graph.device
-        with devtime.span(None, dev):
-            nat.check(nat.lib().ahr_search_host(
-                self.index.handle, self.graph._h, q_host.data_ptr(), B, k_dense, self.row_to_node.data_ptr(),
-                int(self.row_to_node.shape[0]), nat.ctypes.byref(params.to_c_cached()), max_exp, ws.data_ptr(),
-                ws_bytes, out.data_ptr(), nat.stream_ptr(device_index=dev.index)), "ahr_search_host")
+        args = (self.index.handle, *fixed, nat.ctypes.byref(params.to_c_cached()), max_exp, ws.data_ptr(), ws_bytes, out.data_ptr(),
+                nat.stream_ptr(device_index=dev.index))
+        if devtime.active():
+            with devtime.span(None, dev):
+                st = nat.lib().ahr_search_host(*args)
+        else:
+            st = nat.lib().ahr_search_host(*args)
+        nat.check(st, "ahr_search_host")
+        if borrow:  # views of the pinned buffer: valid until the next call (the caller holds the lock)
+            return borrowed
         # one copy of the whole result buffer (the pinned one is the next call's), views into it
-        host = out_np.copy()
-        scores_h, rows_h, *outs = _host_views(host, specs, offs)
+        scores_h, rows_h, *outs = _host_views(out_np.copy(), specs, offs)
         return rows_h, scores_h, RerankResult(*outs)
 
     def _run(self, query_vectors: torch.Tensor, params: RerankParams,

@@ -47,6 +47,7 @@ def main():
         "resolve_search_params": per_call(lambda: resolve_search_params(sp, 5, 5, *([None] * 7)), a.n),
         "search_engine": per_call(lambda: hg.search_engine(db), a.n),
         "engine.run": per_call(lambda: eng.run(qt, params), a.n),
+        "engine.run(numpy, borrow)": per_call(lambda: eng.run(qv, params, borrow=True), a.n),
         "_assemble": per_call(lambda: hg._assemble(eng, rows[0], scores[0], res, 0, 5, False), a.n),
         "_assemble(return_cluster)": per_call(lambda: hg._assemble(eng, rows[0], scores[0], res, 0, 5, True), a.n),
     }
@@ -55,16 +56,14 @@ def main():
     from ah_rag.graph_search import _host_views
     eng.run(qt, params)
     b = next(iter(eng._hbufs.values()))
-    ws, ws_bytes, q_host, q_np, ob, out_np, specs, offs = b
-    k_dense = specs[0][0][1]
+    ws, ws_bytes, q_np, ob, out_np, specs, offs, fixed, _, q_host = b
     max_exp = specs[2][0][1]
     stream = nat.stream_ptr(device_index=dev.index)
     cp = params.to_c_cached()
     lib = nat.lib()
 
     def bare():
-        lib.ahr_search_host(eng.index.handle, eng.graph._h, q_host.data_ptr(), 1, k_dense, eng.row_to_node.data_ptr(),
-                            int(eng.row_to_node.shape[0]), nat.ctypes.byref(cp), max_exp, ws.data_ptr(), ws_bytes,
+        lib.ahr_search_host(eng.index.handle, *fixed, nat.ctypes.byref(cp), max_exp, ws.data_ptr(), ws_bytes,
                             ob.data_ptr(), stream)
 
     out["native_call"] = per_call(bare, a.n)
