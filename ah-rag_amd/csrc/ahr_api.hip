@@ -1,5 +1,6 @@
 // Error channel and process-level queries of the C ABI (include/ahr.h).
 #include "ahr_common.h"
+#include "ahr_internal.h"
 #include "ahr.h"
 
 #include <stdlib.h>
@@ -80,14 +81,34 @@ int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int
   if (!(skip & 1)) AHR_HIP(hipMemcpyAsync(q, host_q, (size_t)B * dim * 4, hipMemcpyHostToDevice, s));
   float* scores = reinterpret_cast<float*>(a + off[0]);
   int32_t* rows = reinterpret_cast<int32_t*>(a + off[1]);
-  st = ahr_index_query(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream);
+  // the small-batch plan's per-split lists are merged by the rerank kernel itself (one launch and
+  // its gap fewer); AHR_SEARCH_FUSE=0 keeps the merge launch (A/B, bitwise equal)
+  static const bool fuse = [] {
+    const char* e = getenv("AHR_SEARCH_FUSE");
+    return !(e && atoi(e) == 0);
+  }();
+  const uint64_t* lists = nullptr;
+  int n_lists = 0;
+  if (fuse && !(skip & 4))
+    st = ahr::dense_query_lists(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream, &lists,
+                                &n_lists);
+  else
+    st = ahr_index_query(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream);
   if (st != AHR_OK) return st;
-  if (!(skip & 4)) st = ahr_graph_expand_rerank_rows(g, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp,
-                                    reinterpret_cast<int32_t*>(a + off[2]), reinterpret_cast<double*>(a + off[3]),
-                                    reinterpret_cast<int32_t*>(a + off[4]), reinterpret_cast<int32_t*>(a + off[5]),
-                                    reinterpret_cast<int32_t*>(a + off[6]), reinterpret_cast<double*>(a + off[7]),
-                                    reinterpret_cast<double*>(a + off[8]), reinterpret_cast<int32_t*>(a + off[9]),
-                                    stream);
+  int32_t* o2 = reinterpret_cast<int32_t*>(a + off[2]);
+  double* o3 = reinterpret_cast<double*>(a + off[3]);
+  int32_t* o4 = reinterpret_cast<int32_t*>(a + off[4]);
+  int32_t* o5 = reinterpret_cast<int32_t*>(a + off[5]);
+  int32_t* o6 = reinterpret_cast<int32_t*>(a + off[6]);
+  double* o7 = reinterpret_cast<double*>(a + off[7]);
+  double* o8 = reinterpret_cast<double*>(a + off[8]);
+  int32_t* o9 = reinterpret_cast<int32_t*>(a + off[9]);
+  if (lists)
+    st = ahr::graph_rerank_lists(g, lists, n_lists, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp, o2,
+                                 o3, o4, o5, o6, o7, o8, o9, stream);
+  else if (!(skip & 4))
+    st = ahr_graph_expand_rerank_rows(g, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp, o2, o3, o4,
+                                      o5, o6, o7, o8, o9, stream);
   if (st != AHR_OK) return st;
   if (!(skip & 2)) AHR_HIP(hipMemcpyAsync(host_out, a, (size_t)arena, hipMemcpyDeviceToHost, s));
   AHR_HIP(hipStreamSynchronize(s));

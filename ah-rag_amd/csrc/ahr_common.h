@@ -69,4 +69,9 @@ __host__ __device__ __forceinline__ float key_score(uint64_t key) {
   return unord_f32((uint32_t)(key >> 32));
 }
 
+// The drop-in search's one-call path (ahr_search_host): the rerank wave kernel merges the dense
+// stage's per-(query, split) lists itself while a query's lists hold at most this many keys
+// (ahr_graph.hip expand_rerank_wave_kernel<true>; 256 splits x top_k 5 = 1,280 for search()).
+constexpr int kRerankFuseKeys = 2048;
+
 }  // namespace ahr

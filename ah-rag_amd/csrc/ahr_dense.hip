@@ -33,6 +33,7 @@
 #include "ahr.h"
 #include "ahr_dense_common.h"
 #include "ahr_qres.h"
+#include "ahr_internal.h"
 
 #include <algorithm>
 #include <cstring>
@@ -2483,51 +2484,6 @@ __global__ __launch_bounds__(256) void read_rows_kernel(const uint8_t* __restric
 }
 
 
-// One wave merges n_lists (<= 512) sorted lists of k_in keys held in LDS: k rounds of a DPP wave
-// max over the list heads (lane l owns lists l + 64 u), a head advancing by an LDS read, no
-// barrier per output; output j goes to o0 + j (merge_block_kernel and the small kernels' fold).
-__device__ __forceinline__ void walk_lists_lds(const uint64_t* kb, int n_lists, int k_in, int k, int64_t o0,
-                                               float* __restrict__ scores, int32_t* __restrict__ rows,
-                                               uint64_t* __restrict__ keys_out) {
-  const int lane = threadIdx.x & 63;
-  constexpr int kH = 8;  // n_lists <= 512
-  int ptr[kH];
-  uint64_t head[kH];
-#pragma unroll
-  for (int u = 0; u < kH; ++u) {
-    const int l = lane + 64 * u;
-    ptr[u] = 0;
-    head[u] = (l < n_lists && k_in > 0) ? kb[l * k_in] : 0;
-  }
-  uint64_t mine = 0;  // lane j % 64 keeps the j-th winner; flushed in windows of 64 outputs
-  for (int j = 0; j < k; ++j) {
-    uint64_t m = head[0];
-#pragma unroll
-    for (int u = 1; u < kH; ++u) m = max_u64(m, head[u]);
-    const uint64_t best = wave_max_u64(m);
-    if (best != 0 && m == best) {
-#pragma unroll
-      for (int u = 0; u < kH; ++u) {
-        if (head[u] == best) {
-          const int l = lane + 64 * u;
-          ++ptr[u];
-          head[u] = ptr[u] < k_in ? kb[l * k_in + ptr[u]] : 0;
-        }
-      }
-    }
-    if (lane == (j & 63)) mine = best;
-    if ((j & 63) == 63 || j == k - 1) {
-      const int j0 = j & ~63;
-      if (j0 + lane <= j) {
-        const int64_t o = o0 + j0 + lane;
-        if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
-        if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
-        if (keys_out) keys_out[o] = mine;
-      }
-    }
-  }
-}
-
 // Small-batch fold (B <= kFoldMaxQ): every workgroup of a small-batch launch publishes its
 // per-(query, split) lists and arrives on a counter in the query workspace; the LAST to arrive
 // merges the n_splits lists of each query (walk_lists_lds) and writes the outputs, so a single
@@ -4127,7 +4083,9 @@ int run_query_large_k(ahr_index* ix, int B, int k, uint32_t row_base, float* sco
 }
 
 int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int64_t row_base,
-              float* scores, int32_t* rows, uint64_t* keys, void* stream) {
+              float* scores, int32_t* rows, uint64_t* keys, void* stream, const uint64_t** lists_out = nullptr,
+              int* n_lists_out = nullptr) {
+  if (lists_out) *lists_out = nullptr;
   if (!ix) return fail(AHR_EINVAL, "null index");
   if (B < 0 || k <= 0) return fail(AHR_EINVAL, "B must be >= 0 and k > 0");
   if (k > AHR_MAX_K_LARGE) return fail(AHR_EUNSUP, "k exceeds AHR_MAX_K_LARGE (4096)");
@@ -4228,7 +4186,15 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
     // qkv: one list per (split, dimension half); t256 / kb256: one per (split, row half)
     const int lists = (cand_plan ? 2 : 1) *
                       p.n_splits;
-    launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
+    // (dense_query_lists: a small-batch plan's lists go to the caller's fused merge instead; not
+    // while stage events are being recorded, whose merge stage would be empty)
+    if (lists_out && ix->count > 0 && p.kernel == KERNEL_SMALL && row_base == 0 &&
+        (int64_t)lists * k <= kRerankFuseKeys && lists <= 512 && ix->prof_calls >= ix->prof_max_calls) {
+      *lists_out = ix->part;
+      *n_lists_out = lists;
+    } else {
+      launch_merge(ix->part, B, ix->count > 0 ? lists : 0, k, k, scores, rows, keys, s);
+    }
   }
   // the next register-resident launch of another stream waits for this batch's merge
   if (p.kernel == KERNEL_QRES && !qres_chain_at_kernel() && (st = qres_chain_record(ix, s))) return st;
@@ -4239,6 +4205,16 @@ int run_query(ahr_index* ix, const float* q, int B, int k, int normalize_q, int6
 }
 
 }  // namespace
+
+namespace ahr {
+
+int dense_query_lists(ahr_index* ix, const float* q, int B, int k, int normalize_q, float* scores, int32_t* rows,
+                      void* stream, const uint64_t** lists, int* n_lists) {
+  if (!scores || !rows || !lists || !n_lists) return fail(AHR_EINVAL, "null output");
+  return run_query(ix, q, B, k, normalize_q, 0, scores, rows, nullptr, stream, lists, n_lists);
+}
+
+}  // namespace ahr
 
 extern "C" {
 

@@ -298,5 +298,53 @@ constexpr uint32_t kKnownFlags = (kKernelFlags & (kAblation ? ~0u : ~(uint32_t)k
                                  kFlagXcdBalance | kFlagNoXcdBalance | kFlagQresMute;
 // every flag but kFlagXcdRemap is an ablation switch (ahr_index_set_debug_flags)
 
+// One wave merges n_lists (<= 512) sorted lists of k_in keys held in LDS: k rounds of a DPP wave
+// max over the list heads (lane l owns lists l + 64 u), a head advancing by an LDS read, no
+// barrier per output; output j goes to o0 + j (merge_block_kernel, the small kernels' fold and
+// the drop-in search's fused rerank, ahr_graph.hip).
+// Returns, for k <= 64, output j in lane j (0 past k).
+__device__ __forceinline__ uint64_t walk_lists_lds(const uint64_t* kb, int n_lists, int k_in, int k, int64_t o0,
+                                                   float* __restrict__ scores, int32_t* __restrict__ rows,
+                                                   uint64_t* __restrict__ keys_out) {
+  const int lane = threadIdx.x & 63;
+  constexpr int kH = 8;  // n_lists <= 512
+  int ptr[kH];
+  uint64_t head[kH];
+#pragma unroll
+  for (int u = 0; u < kH; ++u) {
+    const int l = lane + 64 * u;
+    ptr[u] = 0;
+    head[u] = (l < n_lists && k_in > 0) ? kb[l * k_in] : 0;
+  }
+  uint64_t mine = 0;  // lane j % 64 keeps the j-th winner; flushed in windows of 64 outputs
+  for (int j = 0; j < k; ++j) {
+    uint64_t m = head[0];
+#pragma unroll
+    for (int u = 1; u < kH; ++u) m = max_u64(m, head[u]);
+    const uint64_t best = wave_max_u64(m);
+    if (best != 0 && m == best) {
+#pragma unroll
+      for (int u = 0; u < kH; ++u) {
+        if (head[u] == best) {
+          const int l = lane + 64 * u;
+          ++ptr[u];
+          head[u] = ptr[u] < k_in ? kb[l * k_in + ptr[u]] : 0;
+        }
+      }
+    }
+    if (lane == (j & 63)) mine = best;
+    if ((j & 63) == 63 || j == k - 1) {
+      const int j0 = j & ~63;
+      if (j0 + lane <= j) {
+        const int64_t o = o0 + j0 + lane;
+        if (scores) scores[o] = mine ? key_score(mine) : -INFINITY;
+        if (rows) rows[o] = mine ? (int32_t)key_row(mine) : -1;
+        if (keys_out) keys_out[o] = mine;
+      }
+    }
+  }
+  return k <= 64 ? mine : 0;
+}
+
 }  // namespace dense
 }  // namespace ahr

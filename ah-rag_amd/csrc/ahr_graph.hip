@@ -16,6 +16,8 @@
 // Layout in HBM: node_type int8 [n], judge/conf/judge_term/conf_term f64 [n] (NaN = None),
 // 6 CSR lists (int64 offsets [n+1], int32 targets [nnz]) in networkx iteration order.
 #include "ahr_common.h"
+#include "ahr_dense_common.h"
+#include "ahr_internal.h"
 #include "ahr.h"
 
 #include <math.h>
@@ -184,12 +186,19 @@ __global__ __launch_bounds__(64) void expand_rerank_kernel(
 constexpr int kWaveCand = 1024;  // candidates (and dict entries) per query held in LDS
 constexpr int kWaveSeeds = 64;   // one seed per lane
 
+// LISTS (the drop-in search's one-call path, ahr_search_host): the dense stage's per-(query, split)
+// sorted key lists come in instead of its merged top k_seed — the wave merges them first (the walk
+// of merge_block_kernel over the lists in LDS, dense::walk_lists_lds), writes the merged rows and
+// scores where the merge kernel would have (seed_nodes / seed_sem, read back by the host) and
+// takes its seeds from the winners it holds: one launch and one launch gap fewer per search.
+template <bool LISTS>
 __global__ __launch_bounds__(64) void expand_rerank_wave_kernel(
     DevGraph g, const int32_t* __restrict__ seed_nodes, const int32_t* __restrict__ row_map, int64_t n_map,
     const float* __restrict__ seed_sem, int B, int k_seed, ahr_rerank_params p, int max_exp,
     int32_t* __restrict__ exp_nodes, double* __restrict__ exp_sem, int32_t* __restrict__ exp_src,
     int32_t* __restrict__ exp_count, int32_t* __restrict__ out_nodes, double* __restrict__ out_sem,
-    double* __restrict__ out_score, int32_t* __restrict__ out_count) {
+    double* __restrict__ out_score, int32_t* __restrict__ out_count, const uint64_t* __restrict__ lists,
+    int n_lists) {
   __shared__ int32_t c_node[kWaveCand];
   __shared__ int32_t c_src[kWaveCand];  // seed index (>= 0) or -1 - assumed node type (expansion)
   __shared__ double c_sem[kWaveCand];
@@ -200,6 +209,28 @@ __global__ __launch_bounds__(64) void expand_rerank_wave_kernel(
   const int q = blockIdx.x;
   const int lane = threadIdx.x;
   if (q >= B) return;
+  uint64_t won = 0;  // LISTS: this lane's merged key (dense result lane)
+  if constexpr (LISTS) {
+    __shared__ uint64_t kb[kRerankFuseKeys];
+    const int n = n_lists * k_seed;  // <= kRerankFuseKeys (the caller's check)
+    const uint64_t* src = lists + (int64_t)q * n;
+    // every load in flight at once (a load -> LDS store loop waits one memory latency per key)
+    constexpr int kPer = kRerankFuseKeys / 64;
+    uint64_t v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = lane + 64 * u;
+      if (64 * u < n) v[u] = src[i < n ? i : n - 1];  // (64 u < n: wave-uniform)
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = lane + 64 * u;
+      if (i < n) kb[i] = v[u];
+    }
+    __syncthreads();
+    won = dense::walk_lists_lds(kb, n_lists, k_seed, k_seed, (int64_t)q * k_seed, const_cast<float*>(seed_sem),
+                                const_cast<int32_t*>(seed_nodes), nullptr);
+  }
 
   // ---- candidates: lane s owns seed s
   int32_t nid = -1;
@@ -208,9 +239,16 @@ __global__ __launch_bounds__(64) void expand_rerank_wave_kernel(
   double factor = 0.0;
   int64_t b0 = 0;
   if (lane < k_seed) {
-    nid = seed_nodes[(int64_t)q * k_seed + lane];
+    float ss;
+    if constexpr (LISTS) {
+      nid = won ? (int32_t)key_row(won) : -1;
+      ss = won ? key_score(won) : -INFINITY;
+    } else {
+      nid = seed_nodes[(int64_t)q * k_seed + lane];
+      ss = seed_sem[(int64_t)q * k_seed + lane];
+    }
     if (row_map) nid = nid >= 0 && nid < n_map ? row_map[nid] : -1;
-    const float dist = 1.0f - seed_sem[(int64_t)q * k_seed + lane];  // Chroma's float32 distance
+    const float dist = 1.0f - ss;  // Chroma's float32 distance
     sem = 1.0 - (double)dist;
     if (nid >= 0 && nid < g.n_nodes) {
       const int8_t t = g.type[nid];
@@ -952,7 +990,7 @@ static int expand_rerank_impl(ahr_graph* g, const int32_t* seed_nodes, const int
                               const float* seed_sem, int B, int k_seed, const ahr_rerank_params* params,
                               int max_exp, int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
                               int32_t* exp_count, int32_t* out_nodes, double* out_sem, double* out_score,
-                              int32_t* out_count, void* stream) {
+                              int32_t* out_count, void* stream, const uint64_t* lists = nullptr, int n_lists = 0) {
   if (!g || !params) return fail(AHR_EINVAL, "null graph or params");
   if (B < 0 || k_seed < 0 || params->top_k < 0 || params->member_top_m < 0)
     return fail(AHR_EINVAL, "negative size");
@@ -972,11 +1010,19 @@ static int expand_rerank_impl(ahr_graph* g, const int32_t* seed_nodes, const int
     return e && atoi(e) != 0;
   }();
   const int lim_max = fan > 2 ? fan : 2;
-  if (!serial_only && k_seed <= kWaveSeeds && (int64_t)k_seed * (1 + lim_max) <= kWaveCand)
-    hipLaunchKernelGGL(expand_rerank_wave_kernel, dim3((unsigned)B), dim3(64), 0,
+  const bool wave = !serial_only && k_seed <= kWaveSeeds && (int64_t)k_seed * (1 + lim_max) <= kWaveCand;
+  if (lists) {  // the dense stage's unmerged lists: the wave kernel merges them (ahr_search_host)
+    if (!wave || (int64_t)n_lists * k_seed > kRerankFuseKeys || n_lists > 512)
+      return fail(AHR_EINVAL, "fused list merge: lists do not fit the wave kernel");
+    hipLaunchKernelGGL(expand_rerank_wave_kernel<true>, dim3((unsigned)B), dim3(64), 0,
                        reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
                        k_seed, p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
-                       out_score, out_count);
+                       out_score, out_count, lists, n_lists);
+  } else if (wave)
+    hipLaunchKernelGGL(expand_rerank_wave_kernel<false>, dim3((unsigned)B), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
+                       k_seed, p, max_exp, exp_nodes, exp_sem, exp_src, exp_count, out_nodes, out_sem,
+                       out_score, out_count, (const uint64_t*)nullptr, 0);
   else
     hipLaunchKernelGGL(expand_rerank_kernel, dim3((B + 63) / 64), dim3(64), 0,
                        reinterpret_cast<hipStream_t>(stream), g->dg, seed_nodes, row_map, n_map, seed_sem, B,
@@ -1133,3 +1179,17 @@ int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, 
 }
 
 }  // extern "C"
+
+namespace ahr {
+
+int graph_rerank_lists(ahr_graph* g, const uint64_t* lists, int n_lists, int32_t* rows, const int32_t* row_to_node,
+                       int64_t n_rows, float* scores, int B, int k_seed, const ahr_rerank_params* params,
+                       int max_exp, int32_t* exp_nodes, double* exp_sem, int32_t* exp_src, int32_t* exp_count,
+                       int32_t* out_nodes, double* out_sem, double* out_score, int32_t* out_count, void* stream) {
+  if (!lists || n_lists < 1) return fail(AHR_EINVAL, "null or empty lists");
+  if (!row_to_node || n_rows < 0) return fail(AHR_EINVAL, "null row map or negative row count");
+  return expand_rerank_impl(g, rows, row_to_node, n_rows, scores, B, k_seed, params, max_exp, exp_nodes, exp_sem,
+                            exp_src, exp_count, out_nodes, out_sem, out_score, out_count, stream, lists, n_lists);
+}
+
+}  // namespace ahr
