@@ -107,3 +107,30 @@ def test_c5_vec_env_episodes_match_oracle(hotpot_env):
             assert inf[b]["action_mask"] == eps[b].mask()
     assert (kinds[:5] > 0).all(), kinds  # every action kind was exercised
     print(f"C5: {N_ENVS} envs x {STEPS} steps on {G.number_of_nodes()} nodes match the oracle; actions {kinds.tolist()}")
+
+
+def test_search_host_fused_merge_equals_device_path(hotpot_env):
+    """The one-call search path (host queries, ahr_search_host) merges the small-batch plan's 256
+    per-split lists inside the rerank kernel; the device-tensor path launches the merge kernel and
+    then the rerank (ahr_index_query + ahr_graph_expand_rerank_rows). Same rows, scores and result
+    arrays bit for bit, for every small-plan batch (B <= 4) and several top_k (fused up to
+    256 x top_k <= 2,048 keys: top_k 8 is fused, 10 and 16 take the merge launch inside the call)."""
+    import torch
+    from ah_rag.graph_search import resolve_search_params
+    hg, ids, vectors, qv = hotpot_env
+    db = hg.G.graph["vector_index"]["db_path"]
+    eng = hg.search_engine(db)
+    for top_k in (1, 5, 8, 10, 16):
+        params = resolve_search_params(hg.G.graph.get("search_params", {}), top_k, 5, *([None] * 7))
+        for B in (1, 2, 4):
+            q = np.ascontiguousarray(qv[3 * B:4 * B], np.float32)
+            rows_h, scores_h, res_h = eng.run(q, params)  # host path (fused where it fits)
+            rows_d, scores_d, res_d = eng.run(torch.from_numpy(q).cuda(), params)  # device path
+            assert np.array_equal(rows_h, rows_d) and np.array_equal(scores_h.view(np.uint32),
+                                                                      scores_d.view(np.uint32)), (top_k, B)
+            for f in ("exp_nodes", "exp_sem", "exp_src", "exp_count", "out_nodes", "out_sem", "out_score",
+                      "out_count"):
+                a, b = np.asarray(getattr(res_h, f)), np.asarray(getattr(res_d, f))
+                assert a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8)), (top_k, B, f)
+    plan = eng.index.plan(1, 5)
+    assert plan["kernel"] == "small" and plan["n_splits"] * 5 <= 2048, plan
