@@ -13,3 +13,4 @@ bash tools/gpu/profile.sh ${1:-gpurun_out/final}/final_d384 hotpot90k_d384 || ex
 BATCH=1 DT=0 bash tools/gpu/profile.sh ${1:-gpurun_out/final}/final_f32b1 hotpot90k --dtype f32 --batch 1 || exit 1
 BATCH=1024 DT=0 bash tools/gpu/profile.sh ${1:-gpurun_out/final}/final_f32 hotpot90k --dtype f32 || exit 1
 BATCH=64 bash tools/gpu/profile.sh ${1:-gpurun_out/final}/final_b64 hotpot90k --batch 64 || exit 1
+BATCH=1 bash tools/gpu/profile.sh ${1:-gpurun_out/final}/final_b1 hotpot90k --batch 1 || exit 1
