@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--margins", default="0,0.1")
     ap.add_argument("--gemm", action="store_true")
+    ap.add_argument("--only", default="", help="run only this variant (self_seeded | perfect | gemm_only), for "
+                                               "counter passes (rocprofv3 --pmc) of one launch kind")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     spec = {"hotpot90k": HOTPOT_90K, "hotpot90k_d384": CorpusSpec(dim=384), "synth5m": SYNTH_5M}[a.workload]
@@ -54,6 +56,15 @@ def main():
     kth = s[:, 9].contiguous().clone()
     seeds = {m: (kth - float(m)).contiguous() for m in a.margins.split(",")}
     res = {}
+    if a.only:
+        if a.only == "perfect":
+            ix.set_seed(seeds[a.margins.split(",")[0]])
+        elif a.only == "gemm_only":
+            ix.set_debug_flags(2)
+        res[a.only] = [tile_ms(ix, q, 10, a.steps)]
+        print(json.dumps(res), flush=True)
+        ix.close()
+        return
     for _ in range(a.rounds):
         ix.set_seed(None)
         res.setdefault("self_seeded", []).append(tile_ms(ix, q, 10, a.steps))
