@@ -210,3 +210,22 @@ def test_concurrent_search_threads(workdir):
     for t in ts:
         t.join()
     assert not errors, errors[:5]
+
+
+def test_search_results_survive_later_calls(workdir):
+    """search_batch() builds its dicts from views of the engine's reused result buffer (no copy):
+    what a call returned must not change when later calls overwrite that buffer, and the arrays
+    search_arrays() returns are the caller's own."""
+    import copy
+    d, hg = workdir
+    cases = [c for c in _load("search_cases.json")["cases"] if not c.get("include_hyperedges")][:6]
+    first = hg.search(cases[0]["query"], return_cluster=True, **cases[0]["params"])
+    kept = copy.deepcopy(first)
+    _, _, rows, scores, res = hg.search_arrays([cases[0]["query"]], **cases[0]["params"])
+    kept_arrays = [a.copy() for a in (rows, scores, res.out_nodes, res.out_score, res.exp_nodes)]
+    for c in cases[1:]:
+        hg.search(c["query"], return_cluster=c["return_cluster"], **c["params"])
+        hg.search_batch([c["query"]], return_cluster=True, **c["params"])
+    assert _norm(first) == _norm(kept)
+    for a, b in zip((rows, scores, res.out_nodes, res.out_score, res.exp_nodes), kept_arrays):
+        assert np.array_equal(a, b)
