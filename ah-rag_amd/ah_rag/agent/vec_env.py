@@ -375,8 +375,10 @@ class VecAHRAGGymEnv:
         return [1] * N_ACTIONS if ob.sel_n[e] > 0 else [0] * (N_ACTIONS - 1) + [1]
 
     # ---- the gym API, batched ------------------------------------------------------------------
-    def reset(self, queries: Sequence[str], query_vectors: Optional[np.ndarray] = None
-              ) -> Tuple[np.ndarray, LazyInfos]:
+    def reset(self, queries: Sequence[str], query_vectors=None) -> Tuple[np.ndarray, LazyInfos]:
+        """Reset every environment with its query. query_vectors: [n_envs, d] host array or device
+        tensor (an on-device encoder's output goes to the dense search without a host round trip);
+        None encodes the queries with the graph's encoder."""
         E = self.n_envs
         if len(queries) != E:
             raise ValueError("one query per environment")
