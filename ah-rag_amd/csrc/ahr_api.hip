@@ -95,14 +95,40 @@ int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int
   else
     st = ahr_index_query(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream);
   if (st != AHR_OK) return st;
-  int32_t* o2 = reinterpret_cast<int32_t*>(a + off[2]);
-  double* o3 = reinterpret_cast<double*>(a + off[3]);
-  int32_t* o4 = reinterpret_cast<int32_t*>(a + off[4]);
-  int32_t* o5 = reinterpret_cast<int32_t*>(a + off[5]);
-  int32_t* o6 = reinterpret_cast<int32_t*>(a + off[6]);
-  double* o7 = reinterpret_cast<double*>(a + off[7]);
-  double* o8 = reinterpret_cast<double*>(a + off[8]);
-  int32_t* o9 = reinterpret_cast<int32_t*>(a + off[9]);
+  // With the fused merge every output of the rerank kernel — the merged dense rows / scores too — is
+  // written once and never read back, so when host_out is pinned (device-visible) host memory the
+  // kernel writes the results there directly: no result copy (AHR_SEARCH_ZC=0 keeps the copy). (The
+  // round-5 zero-copy form also had the rerank kernel read the dense results from host memory: slower.)
+  static const bool zc = [] {
+    const char* e = getenv("AHR_SEARCH_ZC");
+    return !(e && atoi(e) == 0);
+  }();
+  char* o = a;
+  if (lists && zc && !(skip & 2)) {
+    static thread_local const void* last_host = nullptr;  // the last pinned buffer checked, its device address
+    static thread_local char* last_dev = nullptr;
+    if (host_out != last_host) {
+      hipPointerAttribute_t at{};
+      last_host = host_out;
+      last_dev = hipPointerGetAttributes(&at, host_out) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer
+                     ? static_cast<char*>(at.devicePointer)
+                     : nullptr;
+      (void)hipGetLastError();  // (a pageable buffer's query error is not the call's)
+    }
+    if (last_dev) o = last_dev;
+  }
+  if (o != a) {
+    scores = reinterpret_cast<float*>(o + off[0]);
+    rows = reinterpret_cast<int32_t*>(o + off[1]);
+  }
+  int32_t* o2 = reinterpret_cast<int32_t*>(o + off[2]);
+  double* o3 = reinterpret_cast<double*>(o + off[3]);
+  int32_t* o4 = reinterpret_cast<int32_t*>(o + off[4]);
+  int32_t* o5 = reinterpret_cast<int32_t*>(o + off[5]);
+  int32_t* o6 = reinterpret_cast<int32_t*>(o + off[6]);
+  double* o7 = reinterpret_cast<double*>(o + off[7]);
+  double* o8 = reinterpret_cast<double*>(o + off[8]);
+  int32_t* o9 = reinterpret_cast<int32_t*>(o + off[9]);
   if (lists)
     st = ahr::graph_rerank_lists(g, lists, n_lists, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp, o2,
                                  o3, o4, o5, o6, o7, o8, o9, stream);
@@ -110,7 +136,7 @@ int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int
     st = ahr_graph_expand_rerank_rows(g, rows, row_to_node, n_rows, scores, B, k_dense, params, max_exp, o2, o3, o4,
                                       o5, o6, o7, o8, o9, stream);
   if (st != AHR_OK) return st;
-  if (!(skip & 2)) AHR_HIP(hipMemcpyAsync(host_out, a, (size_t)arena, hipMemcpyDeviceToHost, s));
+  if (o == a && !(skip & 2)) AHR_HIP(hipMemcpyAsync(host_out, a, (size_t)arena, hipMemcpyDeviceToHost, s));
   AHR_HIP(hipStreamSynchronize(s));
   return AHR_OK;
 }
