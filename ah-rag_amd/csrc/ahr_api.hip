@@ -105,17 +105,13 @@ int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int
   }();
   char* o = a;
   if (lists && zc && !(skip & 2)) {
-    static thread_local const void* last_host = nullptr;  // the last pinned buffer checked, its device address
-    static thread_local char* last_dev = nullptr;
-    if (host_out != last_host) {
-      hipPointerAttribute_t at{};
-      last_host = host_out;
-      last_dev = hipPointerGetAttributes(&at, host_out) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer
-                     ? static_cast<char*>(at.devicePointer)
-                     : nullptr;
-      (void)hipGetLastError();  // (a pageable buffer's query error is not the call's)
-    }
-    if (last_dev) o = last_dev;
+    // checked on every call (a cached answer could outlive the buffer: a pageable buffer at a freed
+    // pinned one's address would take device writes)
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, host_out) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+      o = static_cast<char*>(at.devicePointer);
+    else
+      (void)hipGetLastError();  // (a pageable buffer's lookup error is not the call's)
   }
   if (o != a) {
     scores = reinterpret_cast<float*>(o + off[0]);
