@@ -82,14 +82,15 @@ int ahr_search_host(ahr_index* ix, ahr_graph* g, const float* host_q, int B, int
   float* scores = reinterpret_cast<float*>(a + off[0]);
   int32_t* rows = reinterpret_cast<int32_t*>(a + off[1]);
   // the small-batch plan's per-split lists are merged by the rerank kernel itself (one launch and
-  // its gap fewer); AHR_SEARCH_FUSE=0 keeps the merge launch (A/B, bitwise equal)
+  // its gap fewer) when that kernel is the wave one; AHR_SEARCH_FUSE=0 keeps the merge launch (A/B,
+  // bitwise equal)
   static const bool fuse = [] {
     const char* e = getenv("AHR_SEARCH_FUSE");
     return !(e && atoi(e) == 0);
   }();
   const uint64_t* lists = nullptr;
   int n_lists = 0;
-  if (fuse && !(skip & 4))
+  if (fuse && !(skip & 4) && ahr::graph_rerank_fusable(k_dense, params))
     st = ahr::dense_query_lists(ix, reinterpret_cast<const float*>(q), B, k_dense, 0, scores, rows, stream, &lists,
                                 &n_lists);
   else

@@ -986,6 +986,18 @@ int ahr_graph_info(const ahr_graph* g, int64_t* n_nodes, int64_t* n_edges) {
   return AHR_OK;
 }
 
+// one wave per query while its candidates fit the wave kernel's LDS (every search() / env reset
+// shape: k_seed <= 64); the serial kernel otherwise (large top_k or member_top_m).
+// AHR_RERANK_SERIAL=1: always the serial kernel (A/B; both are bitwise equal).
+static bool rerank_on_wave(int k_seed, int member_top_m) {
+  static const bool serial_only = [] {
+    const char* e = getenv("AHR_RERANK_SERIAL");
+    return e && atoi(e) != 0;
+  }();
+  const int lim_max = member_top_m > 2 ? member_top_m : 2;
+  return !serial_only && k_seed <= kWaveSeeds && (int64_t)k_seed * (1 + lim_max) <= kWaveCand;
+}
+
 static int expand_rerank_impl(ahr_graph* g, const int32_t* seed_nodes, const int32_t* row_map, int64_t n_map,
                               const float* seed_sem, int B, int k_seed, const ahr_rerank_params* params,
                               int max_exp, int32_t* exp_nodes, double* exp_sem, int32_t* exp_src,
@@ -1002,15 +1014,7 @@ static int expand_rerank_impl(ahr_graph* g, const int32_t* seed_nodes, const int
     return fail(AHR_EINVAL, "null buffer");
   const ahr_rerank_params p = *params;
   DeviceGuardG dg(g->device);
-  // one wave per query while its candidates fit the wave kernel's LDS (every search() / env reset
-  // shape: k_seed <= 64); the serial kernel otherwise (large top_k). AHR_RERANK_SERIAL=1: always the
-  // serial kernel (A/B; both are bitwise equal).
-  static const bool serial_only = [] {
-    const char* e = getenv("AHR_RERANK_SERIAL");
-    return e && atoi(e) != 0;
-  }();
-  const int lim_max = fan > 2 ? fan : 2;
-  const bool wave = !serial_only && k_seed <= kWaveSeeds && (int64_t)k_seed * (1 + lim_max) <= kWaveCand;
+  const bool wave = rerank_on_wave(k_seed, p.member_top_m);
   if (lists) {  // the dense stage's unmerged lists: the wave kernel merges them (ahr_search_host)
     if (!wave || (int64_t)n_lists * k_seed > kRerankFuseKeys || n_lists > 512)
       return fail(AHR_EINVAL, "fused list merge: lists do not fit the wave kernel");
@@ -1181,6 +1185,10 @@ int ahr_graph_expand_host(ahr_graph* g, int action, const int32_t* host_inputs, 
 }  // extern "C"
 
 namespace ahr {
+
+bool graph_rerank_fusable(int k_seed, const ahr_rerank_params* params) {
+  return params && k_seed >= 0 && params->member_top_m >= 0 && rerank_on_wave(k_seed, params->member_top_m);
+}
 
 int graph_rerank_lists(ahr_graph* g, const uint64_t* lists, int n_lists, int32_t* rows, const int32_t* row_to_node,
                        int64_t n_rows, float* scores, int B, int k_seed, const ahr_rerank_params* params,

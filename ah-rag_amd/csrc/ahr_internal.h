@@ -15,6 +15,11 @@ namespace ahr {
 int dense_query_lists(ahr_index* ix, const float* q, int B, int k, int normalize_q, float* scores, int32_t* rows,
                       void* stream, const uint64_t** lists, int* n_lists);
 
+// Whether a rerank of k_seed seeds under params runs on the wave kernel (the only one that can
+// merge lists); the caller asks before dense_query_lists, since a large member_top_m or top_k (or
+// AHR_RERANK_SERIAL=1) takes the serial kernel, which needs the merged top-k (ahr_graph.hip).
+bool graph_rerank_fusable(int k_seed, const ahr_rerank_params* params);
+
 // ahr_graph_expand_rerank_rows over those lists: the rerank wave kernel merges each query's lists
 // first and writes the merged rows / scores to rows / scores (ahr_graph.hip).
 int graph_rerank_lists(ahr_graph* g, const uint64_t* lists, int n_lists, int32_t* rows, const int32_t* row_to_node,

@@ -114,29 +114,30 @@ def test_search_host_fused_merge_equals_device_path(hotpot_env):
     per-split lists inside the rerank kernel; the device-tensor path launches the merge kernel and
     then the rerank (ahr_index_query + ahr_graph_expand_rerank_rows). Same rows, scores and result
     arrays bit for bit, for every small-plan batch (B <= 4) and several top_k (fused up to
-    256 x top_k <= 2,048 keys: top_k 8 is fused, 10 and 16 take the merge launch inside the call)."""
+    256 x top_k <= 2,048 keys: top_k 8 is fused, 10 and 16 take the merge launch inside the call;
+    a member_top_m too large for the wave kernel takes the merge launch and the serial kernel)."""
     import torch
     from ah_rag.graph_search import resolve_search_params
     hg, ids, vectors, qv = hotpot_env
     db = hg.G.graph["vector_index"]["db_path"]
     eng = hg.search_engine(db)
-    for top_k in (1, 5, 8, 10, 16):
-        params = resolve_search_params(hg.G.graph.get("search_params", {}), top_k, 5, *([None] * 7))
+    for top_k, m in ((1, 5), (5, 5), (8, 5), (10, 5), (16, 5), (8, 200), (2, 600)):
+        params = resolve_search_params(hg.G.graph.get("search_params", {}), top_k, m, *([None] * 7))
         for B in (1, 2, 4):
             q = np.ascontiguousarray(qv[3 * B:4 * B], np.float32)
             rows_h, scores_h, res_h = eng.run(q, params)  # host path (fused where it fits)
             rows_d, scores_d, res_d = eng.run(torch.from_numpy(q).cuda(), params)  # device path
             assert np.array_equal(rows_h, rows_d) and np.array_equal(scores_h.view(np.uint32),
-                                                                      scores_d.view(np.uint32)), (top_k, B)
+                                                                      scores_d.view(np.uint32)), (top_k, m, B)
             # (the arrays are written up to each query's count; past it the buffers hold leftovers)
             assert np.array_equal(res_h.exp_count, res_d.exp_count) and np.array_equal(res_h.out_count,
-                                                                                       res_d.out_count), (top_k, B)
+                                                                                       res_d.out_count), (top_k, m, B)
             for b in range(B):
                 for f, cnt in (("exp_nodes", res_h.exp_count), ("exp_sem", res_h.exp_count),
                                ("exp_src", res_h.exp_count), ("out_nodes", res_h.out_count),
                                ("out_sem", res_h.out_count), ("out_score", res_h.out_count)):
                     n = int(cnt[b])
                     a, d = np.asarray(getattr(res_h, f))[b, :n], np.asarray(getattr(res_d, f))[b, :n]
-                    assert np.array_equal(a.view(np.uint8), d.view(np.uint8)), (top_k, B, b, f)
+                    assert np.array_equal(a.view(np.uint8), d.view(np.uint8)), (top_k, m, B, b, f)
     plan = eng.index.plan(1, 5)
     assert plan["kernel"] == "small" and plan["n_splits"] * 5 <= 2048, plan
