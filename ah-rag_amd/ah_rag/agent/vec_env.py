@@ -63,6 +63,7 @@ class _NodeTable:
             except (TypeError, ValueError):
                 bad[i] = True
         self.feats, self.bad, self.n = feats, bad, n
+        self.has_bad = bool(bad.any())  # (none: the steps skip the per-environment check)
 
 
 class _ObsBatch:
@@ -94,10 +95,22 @@ class _ObsBatch:
         self.search = None  # reset: (engine, params, rows, scores, res, seed_idx, seed_sem, seed_n)
         self.stamp = None   # the graph version the observation was taken on (HierarchicalGraph._graph_stamp)
 
+    _ROWS = ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size", "f_shown")
+
     def copy_rows(self, src: "_ObsBatch") -> None:
         """src's rows into this batch (the defaults of a step: unchanged observations)."""
-        for name in ("kind", "step", "sel", "sel_n", "score", "sem", "seed_n", "s_size", "f_size", "f_shown"):
+        for name in self._ROWS:
             getattr(self, name)[:] = getattr(src, name)
+
+    @classmethod
+    def following(cls, prev: "_ObsBatch") -> "_ObsBatch":
+        """A new batch holding copies of prev's rows (= cls(E) + copy_rows(prev), one pass)."""
+        ob = cls.__new__(cls)
+        for name in cls._ROWS:
+            setattr(ob, name, getattr(prev, name).copy())
+        ob.S_snap = ob.F_snap = ob.alias = ob.prev = ob.search = ob.stamp = None
+        ob.cache = {}
+        return ob
 
 
 class LazyInfos(_SequenceABC):
@@ -202,6 +215,7 @@ class VecAHRAGGymEnv:
         self._bufs = None
         self._st: Optional[np.ndarray] = None
         self._offs: Optional[List[int]] = None
+        self._layout: Dict[str, Tuple[int, int]] = {}
         self._fcap = self._scap = 0
         self._obs: Optional[_ObsBatch] = None
         self._reset_batch: Optional[_ObsBatch] = None
@@ -221,15 +235,11 @@ class VecAHRAGGymEnv:
     # ---- device state ---------------------------------------------------------------------------
     def _part(self, st: np.ndarray, name: str) -> np.ndarray:
         """A part of an environment-state buffer (DeviceGraph.ENV_PARTS) as a numpy view."""
-        from ..graph_search import DeviceGraph
-        E, K = self.n_envs, K_NODES
-        i = DeviceGraph.ENV_PARTS.index(name)
-        o = self._offs[i]
-        size = {"sel": E * K, "F": E * self._fcap, "S": E * self._scap, "vec": E * VEC_DIM, "err": 1}.get(name, E)
+        o, size = self._layout[name]
         v = st[o:o + size]
         if name == "vec":
-            return v.view(np.float32).reshape(E, VEC_DIM)
-        return v.reshape(E, -1) if name in ("sel", "F", "S") else v
+            return v.view(np.float32).reshape(self.n_envs, VEC_DIM)
+        return v.reshape(self.n_envs, -1) if name in ("sel", "F", "S") else v
 
     def _state_rows(self, which: str, e: int) -> List[int]:
         """Environment e's current selection (S) or frontier (F) members, extended node indices."""
@@ -244,6 +254,11 @@ class VecAHRAGGymEnv:
         g = self._engine.graph
         self._fcap, self._scap = fcap, scap
         self._bufs, self._st, self._offs = g.env_buffers(self.n_envs, K_NODES, fcap, scap)
+        # (offset, int32 element count) of every part, resolved once per layout
+        from ..graph_search import DeviceGraph
+        E = self.n_envs
+        sizes = {"sel": E * K_NODES, "F": E * fcap, "S": E * scap, "vec": E * VEC_DIM, "err": 1}
+        self._layout = {name: (self._offs[i], sizes.get(name, E)) for i, name in enumerate(DeviceGraph.ENV_PARTS)}
 
     def _grow_state(self) -> None:
         """Double the frontier / selection capacity, keeping the state (an environment stepped far
@@ -299,7 +314,8 @@ class VecAHRAGGymEnv:
         vec[:, 2] = np.where(full, np.minimum(ob.f_size, 50), 0)
         vec[:, 3] = ob.seed_n
         valid = np.arange(K_NODES)[None, :] < ob.sel_n[:, None]
-        f = tab.feats[np.where(valid, ob.sel, 0)]
+        sel0 = np.where(valid, ob.sel, 0)
+        f = tab.feats[sel0]
         body = vec[:, 4:].reshape(E, K_NODES, NODE_FEATS)
         body[..., 0:4] = f[..., 0:4]
         body[..., 4] = ob.score
@@ -307,9 +323,10 @@ class VecAHRAGGymEnv:
         body[..., 6:8] = f[..., 4:6]
         body[~valid] = 0.0
         out = vec.astype(np.float32)
-        bad = (tab.bad[np.where(valid, ob.sel, 0)] & valid).any(axis=1)
-        for e in np.flatnonzero(bad).tolist():  # unconvertible attributes: the reference's path (raises)
-            out[e] = featurize_observation(self._obs_dict(ob, e), K_NODES)[0]
+        if tab.has_bad:
+            bad = (tab.bad[sel0] & valid).any(axis=1)
+            for e in np.flatnonzero(bad).tolist():  # unconvertible attributes: the reference's path (raises)
+                out[e] = featurize_observation(self._obs_dict(ob, e), K_NODES)[0]
         return out
 
     # ---- lazily built dicts --------------------------------------------------------------------
@@ -444,12 +461,15 @@ class VecAHRAGGymEnv:
         if prev is None:
             raise AssertionError("Call reset() first")
         E = self.n_envs
-        a = np.asarray([int(x) for x in actions], np.int64)
+        if isinstance(actions, np.ndarray) and actions.ndim == 1 and (
+                actions.dtype.kind in "bi" or (actions.dtype.kind == "u" and actions.dtype.itemsize < 8)):
+            a = actions.astype(np.int64)  # (a policy's integer array: int() of each, without the loop)
+        else:
+            a = np.asarray([int(x) for x in actions], np.int64)
         if a.shape != (E,):
             raise ValueError("one action per environment")
         self._cur += 1
-        ob = _ObsBatch(E)
-        ob.copy_rows(prev)  # the defaults: unchanged (aliased) observations
+        ob = _ObsBatch.following(prev)  # the defaults: unchanged (aliased) observations
         ob.search = prev.search
         ob.stamp = self.hg._graph_stamp()
 
@@ -471,18 +491,21 @@ class VecAHRAGGymEnv:
         snap = st.copy()
         kind = self._part(snap, "kind")
         moved = kind > 0
+        moved2 = moved[:, None]
         self._steps[:] = self._part(snap, "step")
-        ob.step[moved] = self._steps[moved]
-        ob.kind[moved] = np.where(kind[moved] == 1, OBS_EXPAND, np.where(kind[moved] == 2, OBS_COMMIT, OBS_DETAILS))
-        ob.sel[moved] = self._part(snap, "sel")[moved]
-        ob.sel_n[moved] = self._part(snap, "sel_n")[moved]
-        ob.score[moved] = 0.0
-        ob.sem[moved] = 0.0
-        ob.seed_n[moved] = self._part(snap, "seed_n")[moved]
+        np.copyto(ob.step, self._steps, where=moved)
+        # kernel kinds 1 / 2 / other -> expansion / commit / details (OBS_EXPAND / OBS_COMMIT /
+        # OBS_DETAILS are 1 / 2 / 3)
+        np.copyto(ob.kind, np.minimum(kind, OBS_DETAILS), where=moved, casting="unsafe")
+        np.copyto(ob.sel, self._part(snap, "sel"), where=moved2)
+        np.copyto(ob.sel_n, self._part(snap, "sel_n"), where=moved)
+        np.copyto(ob.score, 0.0, where=moved2)
+        np.copyto(ob.sem, 0.0, where=moved2)
+        np.copyto(ob.seed_n, self._part(snap, "seed_n"), where=moved)
         sf = moved & (kind != 3)  # expansions and commits show the sets
-        ob.s_size[sf] = self._part(snap, "s_size")[sf]
-        ob.f_size[sf] = self._part(snap, "f_size")[sf]
-        ob.f_shown[sf] = self._part(snap, "f_shown")[sf]
+        np.copyto(ob.s_size, self._part(snap, "s_size"), where=sf)
+        np.copyto(ob.f_size, self._part(snap, "f_size"), where=sf)
+        np.copyto(ob.f_shown, self._part(snap, "f_shown"), where=sf)
         ob.S_snap, ob.F_snap = self._part(snap, "S"), self._part(snap, "F")
         # end_episode, and any action past the five (gym_env.py _apply's last branch), and details of
         # an empty selection: the same observation
@@ -506,10 +529,11 @@ class VecAHRAGGymEnv:
         # observation keeps its own); environments showing a node whose attributes the featurizer
         # cannot convert take the reference's path (featurize_observation on the dict: it raises)
         vecs = self._part(snap, "vec")
-        valid = np.arange(K_NODES)[None, :] < ob.sel_n[:, None]
-        bad = moved & (tab.bad[np.where(valid, ob.sel, 0)] & valid).any(axis=1)
-        for e in np.flatnonzero(bad).tolist():
-            vecs[e] = featurize_observation(self._obs_dict(ob, e), K_NODES)[0]
+        if tab.has_bad:
+            valid = np.arange(K_NODES)[None, :] < ob.sel_n[:, None]
+            bad = moved & (tab.bad[np.where(valid, ob.sel, 0)] & valid).any(axis=1)
+            for e in np.flatnonzero(bad).tolist():
+                vecs[e] = featurize_observation(self._obs_dict(ob, e), K_NODES)[0]
         cur = self._cur.copy()
 
         def info(e: int) -> Dict[str, Any]:

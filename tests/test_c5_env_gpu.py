@@ -98,7 +98,8 @@ def test_c5_vec_env_episodes_match_oracle(hotpot_env):
                 a = 5
             acts.append(a)
             kinds[a] += 1
-        v, r, d, inf = venv.step(acts)
+        # (a list, or a policy's integer array: int64 / int32)
+        v, r, d, inf = venv.step(acts if t % 2 == 0 else np.asarray(acts, np.int64 if t % 4 == 1 else np.int32))
         for b in range(N_ENVS):
             v_want, r_want, d_want, raw_want = eps[b].step(acts[b])
             np.testing.assert_array_equal(v[b], v_want)
