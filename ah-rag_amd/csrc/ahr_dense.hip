@@ -1988,6 +1988,81 @@ void launch_sample_kth(const float* scores, int B, int G, int k, float* thr, hip
     hipLaunchKernelGGL(sample_kth_kernel<kGroupMax / 64>, dim3(B), dim3(64), 0, s, scores, G, k, thr);
 }
 
+// Group maxima of the sampled rows for batches that fill few 128 x 128 tiles (B = 64: 64 tile
+// workgroups on 256 CUs, each a 12-k-tile LDS pipeline, 11 us). One wave per (32-row block,
+// 32-query block) takes its fragments straight from global memory, NKT k-tiles with six in
+// flight, and runs the tile kernel's MFMA chain (same fragments, same k order): its group maxima
+// are bitwise topk_tile_kernel<MODE_GROUPMAX>'s, written to the same slots (group 2 rb + fh).
+template <int DT, int NKT>
+__global__ __launch_bounds__(64) void sample_groupmax_kernel(const uint8_t* __restrict__ corpus,
+                                                            const uint8_t* __restrict__ queries,
+                                                            int64_t row_stride, int n_q, int n_rb,
+                                                            float* __restrict__ score_out, int64_t score_ld) {
+  constexpr int kD = NKT < 6 ? NKT : 6;  // k-tiles in flight (a latency-bound wave: 2 in flight per CU at B = 64)
+  const int lane = threadIdx.x;
+  const int fr = lane & 31;
+  const int fh = lane >> 5;
+  // ids rb and rb + n_rb (n_rb a multiple of 8) stream the same rows on one XCD
+  const int rb = blockIdx.x % n_rb;
+  const int qb = blockIdx.x / n_rb;
+  const int q = qb * 32 + fr;
+  const uint8_t* a_src = corpus + (int64_t)(rb * 32 + fr) * row_stride + fh * 16;
+  const uint8_t* b_src = queries + (int64_t)(q < n_q ? q : n_q - 1) * row_stride + fh * 16;
+  u32x4 fa[kD][4], fb[kD][4];
+  auto load = [&](int slot, int kt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      fa[slot][g] = *reinterpret_cast<const u32x4*>(a_src + kt * kRowBytes + 32 * g);
+      fb[slot][g] = *reinterpret_cast<const u32x4*>(b_src + kt * kRowBytes + 32 * g);
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < kD; ++s) load(s, s);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int s = kt % kD;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) mfma_step<DT>(fa[s][g], fb[s][g], acc);
+    if (kt + kD < NKT) load(s, kt + kD);
+  }
+  float gm = acc[0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) gm = fmaxf(gm, acc[r]);
+  if (q < n_q) score_out[(int64_t)q * score_ld + 2 * rb + fh] = gm;
+}
+
+// true when the wave form took the pre-pass (S rows, a multiple of 256; k-tiles of a built width)
+template <int DT>
+bool launch_sample_groupmax(const uint8_t* corpus, const uint8_t* queries, int64_t row_stride, int n_ktiles,
+                            int S, int B, float* scores, int64_t score_ld, hipStream_t s) {
+  static const bool tile_only = [] {  // A/B: AHR_PREPASS_TILE=1 keeps the 128 x 128 tile pre-pass
+    const char* e = getenv("AHR_PREPASS_TILE");
+    return e && atoi(e) != 0;
+  }();
+  if (tile_only || S % 256 != 0) return false;
+  const int n_rb = S / 32;
+  const dim3 grid((unsigned)(n_rb * ((B + 31) / 32)));
+  switch (n_ktiles) {
+#define AHR_GM_CASE(N)                                                                                            \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL((sample_groupmax_kernel<DT, N>), grid, dim3(64), 0, s, corpus, queries, row_stride, B, n_rb, \
+                       scores, score_ld);                                                                        \
+    return true;
+    AHR_GM_CASE(4)
+    AHR_GM_CASE(6)
+    AHR_GM_CASE(8)
+    AHR_GM_CASE(12)
+    AHR_GM_CASE(16)
+    AHR_GM_CASE(24)
+#undef AHR_GM_CASE
+    default:
+      return false;
+  }
+}
+
 // k-way merge when each lane holds one whole list in registers (n_lists <= 64, k_in <= KCAP):
 // no dependent global loads inside the k rounds. One wave per query, 4 queries per 256-thread
 // workgroup (B = 1024: 256 workgroups, not 1024 single-wave ones); a list comes in as 16-B loads
@@ -3933,8 +4008,15 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     float* scores = ix->sample;
     float* t = ix->sample + (int64_t)B * (S / 16);
     const int G = S / 16;  // 16-row groups
-    launch_tile<DT, 8, MODE_GROUPMAX>(ix, S / kTileRows, (int)cdiv(B, kTileQ), 1, S / kTileRows, S, B, k, 0,
-                                      nullptr, scores, G, 0, s);
+    // batches up to 64 queries take the wave form (same group maxima; B = 64: 8.6 vs 11.0 us; at
+    // B = 128 / 256 its per-wave fragment loads re-read the rows 4 / 8 times and it loses: 20.5 /
+    // 32.8 vs 19.4 / 19.8 us for the pre-pass stage, profiles/r06/prepass/)
+    const bool wave_form = B <= 64 &&
+                           launch_sample_groupmax<DT>(ix->rows, ix->qbuf, ix->row_stride,
+                                                      ix->d_pad * ix->elem / kRowBytes, S, B, scores, G, s);
+    if (!wave_form)
+      launch_tile<DT, 8, MODE_GROUPMAX>(ix, S / kTileRows, (int)cdiv(B, kTileQ), 1, S / kTileRows, S, B, k, 0,
+                                        nullptr, scores, G, 0, s);
     launch_sample_kth(scores, B, G, k, t, s);
     thr = t;
   }

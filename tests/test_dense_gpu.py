@@ -271,6 +271,29 @@ def test_lane_kernels_bitwise_equal(cuda, k, sample):
     ix.close()
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("B", [17, 64])
+def test_prepass_wave_form_small_batch(cuda, dtype, B):
+    """B <= 64 seeds from sample_groupmax_kernel (one wave per 32 rows x 32 queries, the tile
+    kernel's MFMA chain): results equal the unseeded scan's, with the sampled rows repeated later
+    in the corpus so the seed ties exactly with later rows' scores."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(77 + B)
+    C = _clustered(rng, 40001, 768)
+    C[20000:28192] = C[:8192]          # exact copies of the sampled rows: seed == later scores
+    Q = C[rng.integers(0, 8192, B)] + 0.01 * rng.standard_normal((B, 768)).astype(np.float32)
+    ix = DenseIndex(768, len(C), dtype=dtype, device=cuda)
+    ix.upsert(C)
+    assert ix.plan(B, 10)["kernel"] != "small"
+    out = {}
+    for sample in (8192, 0):
+        ix.set_sample_rows(sample)
+        out[sample] = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    np.testing.assert_array_equal(out[8192][1], out[0][1])
+    np.testing.assert_array_equal(out[8192][0], out[0][0])
+    ix.close()
+
+
 def test_lane_ties_order_by_row(cuda):
     """Duplicate corpus rows tie exactly: lower row id first, across tiles and splits."""
     from ah_rag.embeddings import DenseIndex
