@@ -3486,6 +3486,10 @@ constexpr int kWideMinBatch = 6144;
 
 // Resident workgroups of the 128x128 tile kernel: 2 per CU (VGPR/LDS limited).
 constexpr int kResidentSlots128 = 256 * 2;
+inline int env_int_clamped(const char* name, int dflt, int lo, int hi) {
+  const char* e = getenv(name);
+  return e ? std::max(lo, std::min(hi, atoi(e))) : dflt;
+}
 
 // The query-resident kernel keeps a 128-query block's fragments in registers: bf16/f16 and the
 // dimensions it is instantiated for (d_pad = 384, 768). Its admission threshold is the pre-pass
@@ -3719,7 +3723,10 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   // One wave of workgroups: at most the resident slots, splits rounded DOWN to a multiple of 8
   // (an extra workgroup would run as a second wave) so the XCD remap keeps a split's query
   // blocks on one XCD; the kernel balances tile ranges over the splits.
-  int want = std::max(1, kResidentSlots128 / p.qblocks);
+  // (A/B: AHR_TILE_SLOTS, 8..512, caps the workgroups of the 128 x 128 plans; the workspace is
+  // sized for 512)
+  static const int slots = env_int_clamped("AHR_TILE_SLOTS", kResidentSlots128, 8, kResidentSlots128);
+  int want = std::max(1, slots / p.qblocks);
   want = std::min(want, std::max(1, p.n_row_tiles));
   p.xcd_remap = want >= 8;
   p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
