@@ -3633,6 +3633,19 @@ int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
   return AHR_OK;
 }
 
+// Workgroup cap of the 128 x 128 plans. Two per CU serve one batch at a time best; when the
+// caller keeps batches in flight on several query workspaces (ahr_index_set_workspace: another
+// slot holds a reserved one), one per CU lets two batches' workgroups co-reside: B = 64 / 128 /
+// 256 two in flight 0.0388 / 0.0428 / 0.0594 -> 0.0374 / 0.0401 / 0.0545 ms per step, while one
+// at a time would lose 5 / 1 / 16 % (profiles/r06/slots/). AHR_TILE_SLOTS (8..512) fixes the cap.
+inline int tile_slots(const ahr_index* ix) {
+  static const int fixed = env_int_clamped("AHR_TILE_SLOTS", 0, 0, kResidentSlots128);
+  if (fixed) return std::max(8, fixed);
+  for (int w = 0; w < kMaxWorkspaces; ++w)
+    if (w != ix->cur_ws && ix->parked[w].part_cap > 0) return kResidentSlots128 / 2;
+  return kResidentSlots128;
+}
+
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   SearchPlan p;
   p.kernel = KERNEL_TILE128;
@@ -3723,10 +3736,7 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   // One wave of workgroups: at most the resident slots, splits rounded DOWN to a multiple of 8
   // (an extra workgroup would run as a second wave) so the XCD remap keeps a split's query
   // blocks on one XCD; the kernel balances tile ranges over the splits.
-  // (A/B: AHR_TILE_SLOTS, 8..512, caps the workgroups of the 128 x 128 plans; the workspace is
-  // sized for 512)
-  static const int slots = env_int_clamped("AHR_TILE_SLOTS", kResidentSlots128, 8, kResidentSlots128);
-  int want = std::max(1, slots / p.qblocks);
+  int want = std::max(1, tile_slots(ix) / p.qblocks);
   want = std::min(want, std::max(1, p.n_row_tiles));
   p.xcd_remap = want >= 8;
   p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
