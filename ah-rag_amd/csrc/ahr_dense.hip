@@ -3637,10 +3637,13 @@ int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
 // caller keeps batches in flight on several query workspaces (ahr_index_set_workspace: another
 // slot holds a reserved one), one per CU lets two batches' workgroups co-reside: B = 64 / 128 /
 // 256 two in flight 0.0388 / 0.0428 / 0.0594 -> 0.0374 / 0.0401 / 0.0545 ms per step, while one
-// at a time would lose 5 / 1 / 16 % (profiles/r06/slots/). AHR_TILE_SLOTS (8..512) fixes the cap.
-inline int tile_slots(const ahr_index* ix) {
+// at a time would lose 5 / 1 / 16 % (profiles/r06/slots/). Up to 2 query blocks (B <= 256): at
+// B = 1024 fp32 (8 blocks) one per CU measured 0.4 % slower (profiles/r06/slots_f32/).
+// AHR_TILE_SLOTS (8..512) fixes the cap.
+inline int tile_slots(const ahr_index* ix, int qblocks) {
   static const int fixed = env_int_clamped("AHR_TILE_SLOTS", 0, 0, kResidentSlots128);
   if (fixed) return std::max(8, fixed);
+  if (qblocks > 2) return kResidentSlots128;
   for (int w = 0; w < kMaxWorkspaces; ++w)
     if (w != ix->cur_ws && ix->parked[w].part_cap > 0) return kResidentSlots128 / 2;
   return kResidentSlots128;
@@ -3736,7 +3739,7 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   // One wave of workgroups: at most the resident slots, splits rounded DOWN to a multiple of 8
   // (an extra workgroup would run as a second wave) so the XCD remap keeps a split's query
   // blocks on one XCD; the kernel balances tile ranges over the splits.
-  int want = std::max(1, tile_slots(ix) / p.qblocks);
+  int want = std::max(1, tile_slots(ix, p.qblocks) / p.qblocks);
   want = std::min(want, std::max(1, p.n_row_tiles));
   p.xcd_remap = want >= 8;
   p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
