@@ -3637,13 +3637,13 @@ int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
 // caller keeps batches in flight on several query workspaces (ahr_index_set_workspace: another
 // slot holds a reserved one), one per CU lets two batches' workgroups co-reside: B = 64 / 128 /
 // 256 two in flight 0.0388 / 0.0428 / 0.0594 -> 0.0374 / 0.0401 / 0.0545 ms per step, while one
-// at a time would lose 5 / 1 / 16 % (profiles/r06/slots/). Up to 2 query blocks (B <= 256): at
-// B = 1024 fp32 (8 blocks) one per CU measured 0.4 % slower (profiles/r06/slots_f32/).
-// AHR_TILE_SLOTS (8..512) fixes the cap.
+// at a time would lose 5 / 1 / 16 % (profiles/r06/slots/); B = 384: 0.0768 -> 0.0721 ms
+// (profiles/r06/inflight/). Up to 3 query blocks (B <= 384): at B = 1024 fp32 (8 blocks) one per
+// CU measured 0.4 % slower (profiles/r06/slots_f32/). AHR_TILE_SLOTS (8..512) fixes the cap.
 inline int tile_slots(const ahr_index* ix, int qblocks) {
   static const int fixed = env_int_clamped("AHR_TILE_SLOTS", 0, 0, kResidentSlots128);
   if (fixed) return std::max(8, fixed);
-  if (qblocks > 2) return kResidentSlots128;
+  if (qblocks > 3) return kResidentSlots128;
   for (int w = 0; w < kMaxWorkspaces; ++w)
     if (w != ix->cur_ws && ix->parked[w].part_cap > 0) return kResidentSlots128 / 2;
   return kResidentSlots128;
@@ -4031,7 +4031,10 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
     // batches up to 64 queries take the wave form (same group maxima; B = 64: 8.6 vs 11.0 us; at
     // B = 128 / 256 its per-wave fragment loads re-read the rows 4 / 8 times and it loses: 20.5 /
     // 32.8 vs 19.4 / 19.8 us for the pre-pass stage, profiles/r06/prepass/)
-    const bool wave_form = B <= 64 &&
+    // (A/B: AHR_PREPASS_WAVE_B; two in flight the wave form loses at B = 96 / 128 too: 0.0392 /
+    // 0.0432 vs 0.0385 / 0.0404 ms per step, profiles/r06/inflight/)
+    static const int wave_max_b = env_int_clamped("AHR_PREPASS_WAVE_B", 64, 0, 256);
+    const bool wave_form = B <= wave_max_b &&
                            launch_sample_groupmax<DT>(ix->rows, ix->qbuf, ix->row_stride,
                                                       ix->d_pad * ix->elem / kRowBytes, S, B, scores, G, s);
     if (!wave_form)
