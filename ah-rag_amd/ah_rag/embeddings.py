@@ -352,7 +352,7 @@ class DenseIndex:
         nat.check(nat.lib().ahr_index_set_debug_flags(self._h, flags), "ahr_index_set_debug_flags")
 
     _KERNELS = ("tile128", "lane256", "(retired)", "tilelane128", "(retired)", "qkv128", "t256", "small", "kb256",
-                "(retired)", "qres256")
+                "(retired)", "qres256", "lane64")
 
     def plan(self, batch: int, k: int = 10) -> dict:
         """Launch geometry of a query of this batch size and top-k (diagnostics)."""

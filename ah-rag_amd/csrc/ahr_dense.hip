@@ -3470,7 +3470,16 @@ inline void prof_mark(ahr_index* ix, int stage, hipStream_t s) {
 // register-resident kernel (ahr_qres.hip). Ids 2, 4 and 9 were measured-slower variants (lane
 // 256x128, a one-wave-per-SIMD query-resident kernel, k-blocked 256x128): removed.
 enum { KERNEL_TILE128 = 0, KERNEL_LANE256 = 1, KERNEL_TILELANE = 3, KERNEL_QKV = 5, KERNEL_T256 = 6,
-       KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_QRES = 10 };
+       KERNEL_SMALL = 7, KERNEL_KB256 = 8, KERNEL_QRES = 10, KERNEL_LANE64 = 11 };
+// 256 x 64 lane-local tiles for 17 <= B <= 64 (bf16 / f16): the 128-query tile would multiply
+// half padding (A/B: AHR_LANE64)
+inline bool lane64_on() {
+  static const bool on = [] {
+    const char* e = getenv("AHR_LANE64");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
 
 struct SearchPlan {
   int kernel;
@@ -3718,8 +3727,20 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
   if (k <= 16 && !(ix->debug_flags & kFlagTile128)) {
     if (B >= kWideMinBatch && !(ix->debug_flags & kFlagTileLane))
       p.kernel = KERNEL_LANE256;
+    else if (B <= 64 && ix->dtype != DT_F32 && !(ix->debug_flags & kFlagTileLane) && lane64_on())
+      p.kernel = KERNEL_LANE64;
     else
       p.kernel = KERNEL_TILELANE;
+  }
+  if (p.kernel == KERNEL_LANE64) {
+    p.qblocks = (int)cdiv(B, 64);
+    p.n_row_tiles = (int)cdiv(ix->count, 256);
+    int want = std::max(1, tile_slots(ix, p.qblocks) / p.qblocks);
+    want = std::min(want, std::max(1, p.n_row_tiles));
+    p.xcd_remap = want >= 8;
+    p.n_splits = p.xcd_remap ? want / 8 * 8 : want;
+    p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
+    return p;
   }
   if (p.kernel == KERNEL_LANE256) {
     // 256 x 256 tiles, one resident workgroup per CU. One wave of workgroups; splits a multiple of
@@ -4103,6 +4124,12 @@ void launch_search(ahr_index* ix, const SearchPlan& p, int B, int k, uint32_t ro
   if (p.kernel == KERNEL_LANE256) {
     launch_lane_k<DT, 8, 1, 1, 8, 4, 1>(ix, p, n, B, k, row_base, thr, flags, s);
     return;
+  }
+  if constexpr (DT != DT_F32) {
+    if (p.kernel == KERNEL_LANE64) {  // NB 4, BJ 1, WR 2, WQ 2: 256 rows x 64 queries, 4 waves, 3 stages
+      launch_lane_k<DT, 4, 1, 2, 2, 3, 2>(ix, p, n, B, k, row_base, thr, flags, s);
+      return;
+    }
   }
   switch (k <= 8 ? 8 : (k <= 12 ? 12 : (k <= 16 ? 16 : 32))) {  // lists sized to k
     case 8: launch_tile<DT, 8, MODE_TOPK>(ix, p.n_splits, p.qblocks, p.tiles_per_split, p.n_row_tiles, n, B, k, row_base, thr, nullptr, 0, flags, s); break;

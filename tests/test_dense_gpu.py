@@ -214,7 +214,7 @@ def test_default_plans(cuda):
     assert ix.plan(1024, 13)["kernel"] == "tilelane128"
     assert ix.plan(1, 16)["kernel"] == "small"
     assert ix.plan(16, 10)["kernel"] == "small"
-    assert ix.plan(17, 10)["kernel"] == "tilelane128"
+    assert ix.plan(17, 10)["kernel"] in ("tilelane128", "lane64")
     assert ix.plan(1, 17)["kernel"] == "tile128"
     assert ix.plan(2048, 10)["kernel"] == "qres256"
     assert ix.plan(6144, 10)["kernel"] == "qres256"
@@ -292,6 +292,28 @@ def test_prepass_wave_form_small_batch(cuda, dtype, B):
     np.testing.assert_array_equal(out[8192][1], out[0][1])
     np.testing.assert_array_equal(out[8192][0], out[0][0])
     ix.close()
+
+
+@pytest.mark.parametrize("dtype,d,B", [("bf16", 768, 64), ("bf16", 768, 17), ("f16", 384, 40), ("bf16", 100, 64)])
+def test_lane64_equals_tilelane(cuda, dtype, d, B):
+    """The 256 x 64 lane-local plan (17 <= B <= 64, half precision) chains the same k-ordered MFMA
+    steps as the 128 x 128 one: bitwise equal results (flag 32 forces the 128 x 128 plan)."""
+    from ah_rag.embeddings import DenseIndex
+    rng = np.random.default_rng(91 + B + d)
+    C = _clustered(rng, 40001, d)
+    Q = _clustered(rng, B, d)
+    ix = DenseIndex(d, len(C), dtype=dtype, device=cuda)
+    ix.upsert(C)
+    if ix.plan(B, 10)["kernel"] != "lane64":
+        ix.close()
+        pytest.skip("lane64 plan not selected in this build / setting")
+    a = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    ix.set_debug_flags(32)
+    assert ix.plan(B, 10)["kernel"] == "tilelane128"
+    b = [t.cpu().numpy() for t in ix.query(Q, 10)]
+    ix.close()
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0], b[0])
 
 
 def test_lane_ties_order_by_row(cuda):
@@ -493,7 +515,7 @@ def test_small_plans(cuda):
     ix.set_debug_flags(32)  # an explicit kernel flag overrides the small-batch plan
     assert ix.plan(1, 10)["kernel"] == "tilelane128"
     ix.set_debug_flags(0)
-    assert ix.plan(17, 10)["kernel"] == "tilelane128"
+    assert ix.plan(17, 10)["kernel"] in ("tilelane128", "lane64")
     ix.close()
 
 
