@@ -3649,13 +3649,18 @@ int ensure_qbuf_kb(ahr_index* ix, hipStream_t s) {
 // at a time would lose 5 / 1 / 16 % (profiles/r06/slots/); B = 384: 0.0768 -> 0.0721 ms
 // (profiles/r06/inflight/). Up to 3 query blocks (B <= 384): at B = 1024 fp32 (8 blocks) one per
 // CU measured 0.4 % slower (profiles/r06/slots_f32/). AHR_TILE_SLOTS (8..512) fixes the cap.
+// true when another query workspace slot holds a reserved workspace: the caller keeps batches in
+// flight on several streams
+inline bool concurrent_workspaces(const ahr_index* ix) {
+  for (int w = 0; w < kMaxWorkspaces; ++w)
+    if (w != ix->cur_ws && ix->parked[w].part_cap > 0) return true;
+  return false;
+}
 inline int tile_slots(const ahr_index* ix, int qblocks) {
   static const int fixed = env_int_clamped("AHR_TILE_SLOTS", 0, 0, kResidentSlots128);
   if (fixed) return std::max(8, fixed);
   if (qblocks > 3) return kResidentSlots128;
-  for (int w = 0; w < kMaxWorkspaces; ++w)
-    if (w != ix->cur_ws && ix->parked[w].part_cap > 0) return kResidentSlots128 / 2;
-  return kResidentSlots128;
+  return concurrent_workspaces(ix) ? kResidentSlots128 / 2 : kResidentSlots128;
 }
 
 SearchPlan plan_search(const ahr_index* ix, int B, int k) {
@@ -3677,13 +3682,15 @@ SearchPlan plan_search(const ahr_index* ix, int B, int k) {
     p.qblocks = 1;
     const bool f32 = ix->dtype == AHR_F32;  // 64-row items (a row per lane) vs 16-row blocks
     p.n_row_tiles = (int)cdiv(ix->count, f32 ? 64 : 16);
-    // AHR_SMALL_SPLITS (A/B): workgroups per launch, up to 512 (two per CU co-reside: <= 128 VGPRs)
-    static const int split_env = [] {
-      const char* e = getenv("AHR_SMALL_SPLITS");
-      return e ? std::max(1, std::min(512, atoi(e))) : 256;
-    }();
+    // AHR_SMALL_SPLITS (A/B): workgroups per launch, up to 512 (two per CU co-reside: <= 128 VGPRs).
+    // Unset: 256, or 128 with batches in flight on several workspaces at fp32 B = 4 / half B = 16
+    // (two in flight 0.0672 -> 0.0500 / 0.0352 -> 0.0336 ms per step; one at a time they would
+    // lose 0.075 -> 0.095 / 0.045 -> 0.054 ms; at B = 1 256 stays best: profiles/r06/small_splits/)
+    static const int split_env = env_int_clamped("AHR_SMALL_SPLITS", 0, 0, 512);
+    const int splits = split_env ? split_env
+                                 : (B >= (f32 ? 4 : 16) && concurrent_workspaces(ix) ? 128 : 256);
     p.n_splits = (int)std::max<int64_t>(
-        1, std::min<int64_t>(split_env, cdiv(p.n_row_tiles, f32 ? smallf32::waves_per_split() : small::waves(1))));
+        1, std::min<int64_t>(splits, cdiv(p.n_row_tiles, f32 ? smallf32::waves_per_split() : small::waves(1))));
     p.tiles_per_split = (int)cdiv(p.n_row_tiles, p.n_splits);
     p.xcd_remap = false;
     return p;
