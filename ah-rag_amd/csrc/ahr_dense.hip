@@ -3660,6 +3660,10 @@ inline int tile_slots(const ahr_index* ix, int qblocks) {
   static const int fixed = env_int_clamped("AHR_TILE_SLOTS", 0, 0, kResidentSlots128);
   if (fixed) return std::max(8, fixed);
   if (qblocks > 3) return kResidentSlots128;
+  // fp32, one query block (17 <= B <= 128): one per CU wins one at a time too (B = 64: 0.1965 vs
+  // 0.2325 ms serial; two in flight 0.1637 vs 0.1700; B = 256 two in flight 0.3166 vs 0.3546 ms:
+  // profiles/r06/slots_f32b/)
+  if (ix->dtype == AHR_F32 && qblocks == 1) return kResidentSlots128 / 2;
   return concurrent_workspaces(ix) ? kResidentSlots128 / 2 : kResidentSlots128;
 }
 
